@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident trailer CRC-32 (+ header_crc) over
+batched VAL DATA frames on MI355X (BASELINE.json metric, configs[2] = cfg3:
+1 M DATA frames x 16 KiB payload, header_crc + trailer CRC-32).
+
+One step = one launch of the fused frames kernel over the whole batch already
+resident in HBM. N GPUs (torchrun, one rank per GPU): every rank hashes its
+own 1 M-frame batch (frames are independent -> weak scaling, no collective on
+the data path; the only collectives are the timing barrier/max).
+
+Prints ONE JSON line on rank 0. Extra diagnostics go to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (frames per GPU, payload bytes, explicit offset, header_crc)
+    "cfg3": (1 << 20, 16384, True, True),
+    "cfg2": (1 << 16, 1024, True, False),
+    "cfg4": (131113, 65516, True, False),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--verify", action="store_true", help="time the RX verify kernel instead of TX")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--host-inclusive", action="store_true", help="also time H2D+kernel+D2H (stderr)")
+    return ap.parse_args()
+
+
+def make_frames(torch, dev, n, payload, explicit, first_index, seed):
+    """Synthetic DATA frames laid out like the reference sender's output
+    (src/val_core.c:733-834): [5, flags, LE16 content_len, LE32 0,
+    LE64 offset (explicit), payload, LE32 trailer], packed back to back."""
+    content = payload + (8 if explicit else 0)
+    flen = 8 + content
+    stride = flen + 4
+    g = torch.Generator(device=dev).manual_seed(seed)
+    buf = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device=dev, generator=g)
+    buf[:, 0] = 5
+    buf[:, 1] = 1 if explicit else 0
+    buf[:, 2] = content & 0xFF
+    buf[:, 3] = content >> 8
+    buf[:, 4:8] = 0
+    if explicit:
+        offs = (torch.arange(n, device=dev, dtype=torch.int64) + first_index) * payload
+        buf[:, 8:16] = offs.view(torch.uint8).view(n, 8)
+    buf[:, flen:] = 0
+    return buf, flen, stride
+
+
+def cpu_baseline(sample: np.ndarray, stride: int, flen: int, n: int, threads: int):
+    """Time the reference's own val_crc32 (oracle/_ref, built from
+    /root/reference/src) -- or the oracle port if that build is absent --
+    over a host copy of `n` frames of the same workload."""
+    kind = "reference"
+    so = os.path.join(ROOT, "oracle", "_ref", "libref_bench.so")
+    out = np.zeros(n, np.uint32)
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        fn = lib.ref_bench_frames
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                       ctypes.c_int]
+        run = lambda: fn(sample.ctypes.data, stride, flen, n, out.ctypes.data, threads)  # noqa: E731
+    else:
+        kind = "port"
+        from tests import _oracle
+
+        run = lambda: _oracle.lib().oracle_crc32_frames_strided(sample.ctypes.data, stride, flen, n,  # noqa: E731
+                                                                out.ctypes.data, None, threads)
+    run()  # warm caches/pages
+    reps, t_total = 0, 0.0
+    while True:  # accumulate >= ~10 s of CPU (thread) time, <= ~4 s wall
+        t0 = time.perf_counter()
+        run()
+        t_total += time.perf_counter() - t0
+        reps += 1
+        if t_total * threads >= 10.0 or t_total >= 4.0:
+            break
+    gibs = reps * n * flen / t_total / GIB
+    return gibs, kind, out, reps, t_total
+
+
+def read_pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_<config>.json, produced by tools/pmc_traffic.py),
+    or None."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    import val_protocol_amd.crc as vc
+
+    vc.init(local)
+    n, payload, explicit, header = CONFIGS[args.config]
+    buf, flen, stride = make_frames(torch, dev, n, payload, explicit, rank * n, seed=1234 + rank)
+    flat = buf.view(-1)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    if args.verify:  # trailers must be valid first
+        vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc)
+        buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
+
+    def step():
+        if args.verify:
+            vc.verify_frames(flat, stride=stride, flen=flen, n=n, out_ok=ok, nbad=nbad, out_hdr=hdr)
+        else:
+            vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    # Parity spot check of this run's output against the oracle (not timed).
+    sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, 256, replace=False), [0, n - 1]]))
+    rows = buf[torch.from_numpy(sample_idx).to(dev)].cpu().numpy().reshape(-1)
+    from tests import _oracle
+
+    want = _oracle.frames_strided(rows, stride, flen, sample_idx.size)
+    got = crc.cpu().numpy().view(np.uint32)[sample_idx] if not args.verify else want
+    parity = bool(np.array_equal(got, want))
+    if args.verify:
+        parity = parity and int(nbad.item()) == 0
+
+    bytes_per_launch = n * flen  # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
+    total_bytes = bytes_per_launch * args.steps * world
+    value = total_bytes / elapsed_max / GIB
+    achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
+
+    if args.host_inclusive and rank == 0:
+        host = buf.cpu().numpy().reshape(-1)
+        t1 = time.perf_counter()
+        for _ in range(2):
+            vc.frames_host(host, stride=stride, flen=flen, n=n)
+        hi = 2 * bytes_per_launch / (time.perf_counter() - t1) / GIB
+        print(f"[bench] host-inclusive (pageable H2D + kernel + D2H): {hi:.2f} GiB/s", file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        ns = min(n, max(1, (1 << 30) // flen))  # ~1 GiB host sample of the same frames
+        host_rows = buf[:ns].cpu().numpy().reshape(-1)
+        cgibs, kind, cout, reps, tt = cpu_baseline(host_rows, stride, flen, ns, threads)
+        same = bool(np.array_equal(cout, crc[:ns].cpu().numpy().view(np.uint32))) if not args.verify else None
+        cpu = {"value": round(cgibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+               "sample": f"first {ns} frames of this batch ({ns * flen / GIB:.2f} GiB) x{reps} reps, "
+                         f"reference val_crc32 per frame, frames round-robin over {threads} pthreads; "
+                         f"outputs equal GPU: {same}"}
+
+    if rank == 0:
+        metric = "GiB/s device-resident trailer CRC-32 over batched DATA packets, 1 MI355X"
+        line = {
+            "metric": metric,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device-generated random payloads, reference DATA framing)",
+            "config": {
+                "workload": f"{args.config}: {n} DATA frames x {payload} B payload per GPU, "
+                            f"{'header_crc + ' if header else ''}trailer CRC-32"
+                            f"{' (RX verify)' if args.verify else ''}",
+                "frames_per_gpu": n,
+                "crc_input_bytes_per_frame": flen,
+                "frame_stride": stride,
+                "lanes_per_frame": vc.lanes_per_frame(flen),
+                "parallelism": f"frame-sharded x{world} (no collective)",
+                "parity_sample_ok": parity,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel_ms": round(kern_ms, 4),
+                "bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

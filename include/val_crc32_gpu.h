@@ -1,0 +1,112 @@
+/*
+ * val_crc32_gpu.h -- C ABI of the MI355X (gfx950) CRC-32 integrity path.
+ * Exported by val_protocol_amd/libval_crc_hip.so. Plain C types only; HIP
+ * streams travel as `void *` (a hipStream_t, NULL = the library's stream).
+ *
+ * What each entry point replaces in the reference (VAL v0.7):
+ *   val_gpu_crc32_provider  -> a crc32_func_t for val_config_t.crc32_provider
+ *                              (include/val_protocol.h:163-166, :264-266),
+ *                              consumed by val_internal_crc32
+ *                              (src/val_core.c:399-406) and the region CRC
+ *                              (src/val_core.c:431-438)
+ *   val_crc32, val_crc32_{init,update,finalize}_state
+ *                           -> src/val_core.c:150-183 (declared in
+ *                              val_protocol.h)
+ *   val_crc32_frames_*      -> the per-frame trailer CRC of the TX path
+ *                              (src/val_core.c:828-834), batched over a window
+ *                              (src/val_sender.c:822-841); optional header_crc
+ *   val_crc32_verify_frames_* -> the RX trailer check (src/val_core.c:963-974),
+ *                              batched; counts mismatches like crc_errors++
+ *   val_crc32_region_dev    -> val_internal_crc32_region (src/val_core.c:414-455)
+ *                              for resume tail-verify windows up to and beyond
+ *                              256 MiB (src/val_receiver.c:158-181)
+ *   val_crc32_combine/shift -> GF(2) algebra used to split long windows and
+ *                              shard batches across GPUs (no reference
+ *                              counterpart; zlib's crc32_combine identity)
+ *
+ * Every entry point computes on the GPU. There is no CPU fallback: a missing
+ * device or a HIP failure returns VAL_ERR_IO (batch calls) or aborts with a
+ * message (the scalar hooks, whose C signature has no error channel).
+ */
+#ifndef VAL_CRC32_GPU_H
+#define VAL_CRC32_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "val_errors.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAL_GPU_ABI_VERSION 1u
+
+/* ---- lifetime ---------------------------------------------------------- */
+/* Bind the calling process to HIP device `device` (0-based). Idempotent;
+ * lazily called with device 0 by the first CRC call. */
+val_status_t val_gpu_init(int device);
+void val_gpu_shutdown(void);
+int val_gpu_device_count(void);
+uint32_t val_gpu_abi_version(void);
+/* Last HIP/validation error text of the calling thread ("" if none). */
+const char *val_gpu_last_error(void);
+
+/* ---- scalar hooks (host memory) --------------------------------------- */
+uint32_t val_gpu_crc32_provider(uint32_t seed, const void *buf, size_t len);
+uint32_t val_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+/* state * x^(8*nbytes) mod P: advance a raw register over nbytes zero bytes. */
+uint32_t val_crc32_shift(uint32_t state, uint64_t nbytes);
+
+/* ---- batch frames, device-resident (async on `stream`) ------------------
+ * Frame i is the CRC input base[off_i, off_i + len_i):
+ *   descriptor mode: d_off[i], d_len[i] (device arrays; stride/flen ignored)
+ *   strided mode   : d_off == d_len == NULL, off_i = i*stride, len_i = flen
+ * Outputs (device, n entries, any may be NULL):
+ *   d_crc[i] = CRC-32 of frame i (the trailer value)
+ *   d_hdr[i] = header_crc = CRC-32 of the first min(8, len_i) bytes
+ * len_hint: typical frame length, picks the lanes-per-frame geometry in
+ * descriptor mode (0 = 16 KiB). Lengths may be 0 .. 2^32-1.            */
+val_status_t val_crc32_frames_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t stride,
+                                  uint32_t flen, uint32_t n, uint32_t len_hint, uint32_t *d_crc, uint32_t *d_hdr,
+                                  void *stream);
+
+/* RX verify: frame i's stored trailer is the LE32 at base + off_i + len_i.
+ * d_ok[i] = 1 if it equals the recomputed CRC else 0 (nullable);
+ * *d_nbad (device u32, nullable) is INCREMENTED by the number of mismatches
+ * (zero it first; mirrors metrics.crc_errors++). d_crc/d_hdr as above. */
+val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                                         uint64_t stride, uint32_t flen, uint32_t n, uint32_t len_hint, uint8_t *d_ok,
+                                         uint32_t *d_nbad, uint32_t *d_crc, uint32_t *d_hdr, void *stream);
+
+/* Region CRC of one long device buffer: *d_state_out = raw register after
+ * feeding d_ptr[0, len) to `state_in` (val_crc32_update_state semantics;
+ * finalize with ^0xFFFFFFFF). Per-chunk partial states live in stream-ordered
+ * scratch (hipMallocAsync on `stream`), so concurrent calls on different
+ * streams do not share state. */
+val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_state_out,
+                                  void *stream);
+/* Scratch bytes the region call needs for a given length (informational). */
+uint64_t val_crc32_region_scratch_bytes(uint64_t len);
+
+/* ---- batch frames, host memory (synchronous; H2D + kernel + D2H) --------
+ * base_len bounds every frame: off[i] + len[i] (+4 for verify) <= base_len,
+ * else VAL_ERR_INVALID_ARG. off/len NULL = strided mode as above.        */
+val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
+                                   uint64_t stride, uint32_t flen, uint32_t n, uint32_t *crc, uint32_t *hdr);
+val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
+                                          const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint8_t *ok,
+                                          uint32_t *nbad);
+
+/* ---- introspection for benchmarks ---------------------------------------
+ * Lanes per frame the library would pick for a given typical length. */
+uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);
+/* Force the lanes-per-frame geometry (1,2,4,...,64) for later calls of this
+ * process; 0 restores the automatic choice. Returns VAL_ERR_INVALID_ARG for
+ * other values. Results never depend on it; only speed does. */
+val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAL_CRC32_GPU_H */

@@ -1,0 +1,361 @@
+/*
+ * provider_harness.c -- drop-in witness (TEST INFRASTRUCTURE).
+ *
+ * Runs the REFERENCE protocol code (compiled from /root/reference/src into
+ * this binary by oracle/Makefile) with the MI355X provider installed exactly
+ * the way a VAL user would: cfg.crc32_provider = val_gpu_crc32_provider
+ * (reference include/val_protocol.h:264-266). The product library is
+ * dlopen'ed RTLD_LOCAL so none of its symbols can interpose on the
+ * reference's own val_crc32.
+ *
+ *   provider_harness <libval_crc_hip.so> tx
+ *       DATA frames through val_internal_send_packet_ex (src/val_core.c:874)
+ *       with the GPU provider; prints each trailer next to the reference's
+ *       own val_crc32 of the same bytes.
+ *   provider_harness <libval_crc_hip.so> rx
+ *       frames fed to val_internal_recv_packet (src/val_core.c:880) with the
+ *       GPU provider: clean frames -> VAL_OK, corrupted -> VAL_ERR_CRC and
+ *       metrics.crc_errors++.
+ *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
+ *       full val_send_files / val_receive_files transfer over an in-memory
+ *       duplex pipe (the reference test strategy), provider on
+ *       both sessions ("none" = reference built-in CRC). Prints a digest of
+ *       every frame put on the wire so runs can be compared bit for bit.
+ * Output: one JSON object per line.
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "prng.h"
+#include "val_internal.h"
+#include "val_protocol.h"
+#include "val_wire.h"
+
+static crc32_func_t g_gpu;
+static unsigned long g_calls;
+static uint32_t counting_provider(uint32_t seed, const void *buf, size_t len)
+{
+    __atomic_fetch_add(&g_calls, 1, __ATOMIC_RELAXED);
+    return g_gpu(seed, buf, len);
+}
+
+static uint32_t ticks(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint32_t)(ts.tv_sec * 1000u + ts.tv_nsec / 1000000u);
+}
+static void delay(uint32_t ms)
+{
+    struct timespec ts = {ms / 1000u, (long)(ms % 1000u) * 1000000L};
+    nanosleep(&ts, NULL);
+}
+
+/* ---- in-memory byte pipe ------------------------------------------------ */
+typedef struct {
+    uint8_t *buf;
+    size_t cap, head, len;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} pipe_t;
+
+static void pipe_init(pipe_t *p, size_t cap)
+{
+    p->buf = (uint8_t *)malloc(cap);
+    p->cap = cap;
+    p->head = p->len = 0;
+    pthread_mutex_init(&p->mu, NULL);
+    pthread_cond_init(&p->cv, NULL);
+}
+
+static int pipe_push(pipe_t *p, const uint8_t *d, size_t n)
+{
+    pthread_mutex_lock(&p->mu);
+    if (p->len + n > p->cap) {
+        pthread_mutex_unlock(&p->mu);
+        return -1;
+    }
+    for (size_t i = 0; i < n; i++) p->buf[(p->head + p->len + i) % p->cap] = d[i];
+    p->len += n;
+    pthread_cond_broadcast(&p->cv);
+    pthread_mutex_unlock(&p->mu);
+    return (int)n;
+}
+
+static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
+{
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += timeout_ms / 1000u;
+    dl.tv_nsec += (long)(timeout_ms % 1000u) * 1000000L;
+    if (dl.tv_nsec >= 1000000000L) { dl.tv_sec++; dl.tv_nsec -= 1000000000L; }
+    pthread_mutex_lock(&p->mu);
+    while (p->len < n) {
+        if (pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
+            pthread_mutex_unlock(&p->mu);
+            return 0;
+        }
+    }
+    for (size_t i = 0; i < n; i++) d[i] = p->buf[(p->head + i) % p->cap];
+    p->head = (p->head + n) % p->cap;
+    p->len -= n;
+    pthread_mutex_unlock(&p->mu);
+    return 1;
+}
+
+typedef struct {
+    pipe_t *out, *in;
+    uint32_t digest;   /* running CRC (reference val_crc32 state) of all sent bytes */
+    unsigned long frames;
+} end_t;
+
+static int tp_send(void *ctx, const void *data, size_t len)
+{
+    end_t *e = (end_t *)ctx;
+    e->digest = val_crc32_update_state(e->digest, data, len);
+    e->frames++;
+    return pipe_push(e->out, (const uint8_t *)data, len);
+}
+
+static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
+{
+    end_t *e = (end_t *)ctx;
+    if (pipe_pop(e->in, (uint8_t *)buffer, size, timeout_ms)) {
+        if (got) *got = size;
+    } else if (got) {
+        *got = 0;
+    }
+    return 0;
+}
+
+static void *fs_open(void *c, const char *path, const char *mode) { (void)c; return fopen(path, mode); }
+static size_t fs_read(void *c, void *b, size_t s, size_t n, void *f) { (void)c; return fread(b, s, n, (FILE *)f); }
+static size_t fs_write(void *c, const void *b, size_t s, size_t n, void *f) { (void)c; return fwrite(b, s, n, (FILE *)f); }
+static int fs_seek(void *c, void *f, int64_t o, int w) { (void)c; return fseeko((FILE *)f, (off_t)o, w); }
+static int64_t fs_tell(void *c, void *f) { (void)c; return (int64_t)ftello((FILE *)f); }
+static int fs_close(void *c, void *f) { (void)c; return fclose((FILE *)f); }
+
+static void make_cfg(val_config_t *cfg, end_t *e, size_t mtu, crc32_func_t prov)
+{
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->transport.send = tp_send;
+    cfg->transport.recv = tp_recv;
+    cfg->transport.io_context = e;
+    cfg->filesystem.fopen = fs_open;
+    cfg->filesystem.fread = fs_read;
+    cfg->filesystem.fwrite = fs_write;
+    cfg->filesystem.fseek = fs_seek;
+    cfg->filesystem.ftell = fs_tell;
+    cfg->filesystem.fclose = fs_close;
+    cfg->crc32_provider = prov;
+    cfg->system.get_ticks_ms = ticks;
+    cfg->system.delay_ms = delay;
+    cfg->buffers.send_buffer = calloc(1, mtu);
+    cfg->buffers.recv_buffer = calloc(1, mtu);
+    cfg->buffers.packet_size = mtu;
+    cfg->resume.mode = VAL_RESUME_TAIL;
+    cfg->resume.tail_cap_bytes = 1024;
+    cfg->timeouts.min_timeout_ms = 200;
+    cfg->timeouts.max_timeout_ms = 5000;
+    cfg->retries.handshake_retries = 3;
+    cfg->retries.meta_retries = 2;
+    cfg->retries.data_retries = 4;
+    cfg->retries.ack_retries = 6;
+    cfg->retries.backoff_ms_base = 10;
+}
+
+static void hex(const uint8_t *p, size_t n)
+{
+    putchar('"');
+    for (size_t i = 0; i < n; i++) printf("%02x", p[i]);
+    putchar('"');
+}
+
+static int mode_tx(void)
+{
+    const size_t mtu = VAL_MAX_PACKET_SIZE;
+    pipe_t a;
+    pipe_init(&a, 4u << 20);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, counting_provider);
+    val_session_t *s = NULL;
+    if (val_session_create(&cfg, &s, NULL) != VAL_OK) return 2;
+    const uint32_t payloads[] = {0, 1, 3, 492, 1004, 1024, 4093, 16384, 65516, 65527};
+    uint8_t *pl = (uint8_t *)malloc(70000), *w = (uint8_t *)malloc(mtu);
+    for (size_t i = 0; i < sizeof(payloads) / sizeof(payloads[0]); i++)
+        for (int inc = 0; inc <= 1; inc++) {
+            oracle_prng_fill(0xF3u ^ ((uint64_t)payloads[i] << 8), pl, payloads[i]);
+            size_t before = a.len;
+            int rc = val_internal_send_packet_ex(s, VAL_PKT_DATA, pl, payloads[i], (uint64_t)i * 65536u, inc);
+            size_t wl = a.len - before;
+            pipe_pop(&a, w, wl, 10);
+            uint32_t ref = wl >= 12 ? val_crc32(w, wl - 4) : 0u;   /* reference CPU CRC */
+            printf("{\"mode\":\"tx\",\"payload_len\":%u,\"include_offset\":%d,\"rc\":%d,\"wire_len\":%zu,\"header\":", payloads[i],
+                   inc, rc, wl);
+            hex(w, wl >= 8 ? 8 : wl);
+            printf(",\"trailer\":");
+            hex(w + (wl >= 4 ? wl - 4 : 0), wl >= 4 ? 4 : 0);
+            printf(",\"ref_crc\":%u}\n", ref);
+        }
+    printf("{\"mode\":\"tx_summary\",\"provider_calls\":%lu}\n", g_calls);
+    val_session_destroy(s);
+    return 0;
+}
+
+static int mode_rx(void)
+{
+    const size_t mtu = 70000;
+    pipe_t a;
+    pipe_init(&a, 8u << 20);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, counting_provider);
+    val_session_t *s = NULL;
+    if (val_session_create(&cfg, &s, NULL) != VAL_OK) return 2;
+    const uint32_t payloads[] = {0, 7, 1004, 16384, 65516};
+    uint8_t *pl = (uint8_t *)malloc(70000), *out = (uint8_t *)malloc(70000);
+    int idx = 0;
+    for (size_t i = 0; i < sizeof(payloads) / sizeof(payloads[0]); i++)
+        for (int corrupt = 0; corrupt <= 2; corrupt++) {
+            oracle_prng_fill(0xA0u + idx, pl, payloads[i]);
+            /* frame it with the reference TX path (reference CRC: provider off) */
+            cfg.crc32_provider = NULL;
+            val_session_t *txs = NULL;
+            val_session_create(&cfg, &txs, NULL);
+            size_t before = a.len;
+            val_internal_send_packet_ex(txs, VAL_PKT_DATA, pl, payloads[i], 4096u * (uint64_t)idx, 1);
+            size_t wl = a.len - before;
+            val_session_destroy(txs);
+            if (corrupt) {  /* 1: flip a trailer bit, 2: flip a content bit */
+                size_t pos = corrupt == 1 ? a.head + before + wl - 1 : a.head + before + 8u + (wl - 12u) / 2u;
+                a.buf[pos % a.cap] ^= 0x20;
+            }
+            uint32_t plen = 0;
+            uint64_t off = 0;
+            val_packet_type_t t = 0;
+            int rc = val_internal_recv_packet(s, &t, out, 70000, &plen, &off, 100);
+            val_metrics_t m;
+            memset(&m, 0, sizeof m);
+            val_get_metrics(s, &m);
+            int same = (rc == VAL_OK) ? (plen == payloads[i] && memcmp(out, pl, plen) == 0) : 0;
+            printf("{\"mode\":\"rx\",\"payload_len\":%u,\"corrupt\":%d,\"rc\":%d,\"payload_ok\":%d,\"crc_errors\":%u}\n", payloads[i],
+                   corrupt, rc, same, m.crc_errors);
+            idx++;
+        }
+    printf("{\"mode\":\"rx_summary\",\"provider_calls\":%lu}\n", g_calls);
+    val_session_destroy(s);
+    return 0;
+}
+
+typedef struct {
+    val_session_t *rx;
+    const char *dir;
+    val_status_t st;
+} rx_job_t;
+
+static void *rx_main(void *arg)
+{
+    rx_job_t *j = (rx_job_t *)arg;
+    j->st = val_receive_files(j->rx, j->dir);
+    return NULL;
+}
+
+static int mode_loopback(size_t bytes, size_t mtu, int use_gpu)
+{
+    char tmpl[] = "/tmp/valgpuXXXXXX";
+    char *dir = mkdtemp(tmpl);
+    if (!dir) return 2;
+    char in[512], outdir[512], out[512];
+    snprintf(in, sizeof in, "%s/input.bin", dir);
+    snprintf(outdir, sizeof outdir, "%s/out", dir);
+    snprintf(out, sizeof out, "%s/out/input.bin", dir);
+    mkdir(outdir, 0777);
+    uint8_t *data = (uint8_t *)malloc(bytes ? bytes : 1);
+    oracle_prng_fill(0x10AD, data, bytes);
+    FILE *f = fopen(in, "wb");
+    fwrite(data, 1, bytes, f);
+    fclose(f);
+
+    pipe_t a2b, b2a;
+    pipe_init(&a2b, 64u << 20);
+    pipe_init(&b2a, 64u << 20);
+    end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0};
+    crc32_func_t prov = use_gpu ? counting_provider : NULL;
+    val_config_t ctx_, crx;
+    make_cfg(&ctx_, &etx, mtu, prov);
+    make_cfg(&crx, &erx, mtu, prov);
+    val_session_t *tx = NULL, *rx = NULL;
+    if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
+    rx_job_t job = {rx, outdir, VAL_OK};
+    pthread_t th;
+    pthread_create(&th, NULL, rx_main, &job);
+    const char *files[1] = {in};
+    uint32_t t0 = ticks();
+    val_status_t st = val_send_files(tx, files, 1, NULL);
+    pthread_join(th, NULL);
+    uint32_t t1 = ticks();
+    val_metrics_t mt, mr;
+    memset(&mt, 0, sizeof mt);
+    memset(&mr, 0, sizeof mr);
+    val_get_metrics(tx, &mt);
+    val_get_metrics(rx, &mr);
+    int equal = 0;
+    FILE *g = fopen(out, "rb");
+    if (g) {
+        uint8_t *back = (uint8_t *)malloc(bytes + 1);
+        size_t r = fread(back, 1, bytes + 1, g);
+        fclose(g);
+        equal = (r == bytes) && memcmp(back, data, bytes) == 0;
+        free(back);
+    }
+    printf("{\"mode\":\"loopback\",\"gpu\":%d,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,\"rx_status\":%d,\"equal\":%d,"
+           "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"provider_calls\":%lu,\"wall_ms\":%u}\n",
+           use_gpu, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
+           mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu, g_calls, t1 - t0);
+    val_session_destroy(tx);
+    val_session_destroy(rx);
+    remove(out);
+    remove(in);
+    rmdir(outdir);
+    rmdir(dir);
+    return 0;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s <libval_crc_hip.so|none> tx|rx|loopback [bytes mtu]\n", argv[0]);
+        return 1;
+    }
+    int use_gpu = strcmp(argv[1], "none") != 0;
+    if (use_gpu) {
+        void *h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            fprintf(stderr, "dlopen: %s\n", dlerror());
+            return 1;
+        }
+        g_gpu = (crc32_func_t)dlsym(h, "val_gpu_crc32_provider");
+        int (*init)(int) = (int (*)(int))dlsym(h, "val_gpu_init");
+        if (!g_gpu || !init || init(0) != 0) {
+            fprintf(stderr, "GPU provider unavailable\n");
+            return 1;
+        }
+        (void)g_gpu(0xFFFFFFFFu, "warm", 4); /* first call pays HIP init, not the protocol */
+        g_calls = 0;
+    }
+    if (!strcmp(argv[2], "tx")) return use_gpu ? mode_tx() : 1;
+    if (!strcmp(argv[2], "rx")) return use_gpu ? mode_rx() : 1;
+    if (!strcmp(argv[2], "loopback") && argc >= 5)
+        return mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu);
+    fprintf(stderr, "bad mode\n");
+    return 1;
+}

@@ -1,0 +1,75 @@
+"""The drop-in boundary: the C-ABI library loads, exports every function the
+public headers declare, and the public struct layout equals the reference's
+(golden abi block, measured on the reference headers)."""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+import val_protocol_amd.crc as vc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+
+
+def _declared_functions():
+    names = set()
+    for h in ("val_crc32_gpu.h", "val_protocol.h", "val_wire.h"):
+        txt = open(os.path.join(INC, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        txt = re.sub(r"static inline[^{]*\{[^}]*\}", "", txt)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*\b(val_[a-z0-9_]+)\s*\(", txt, re.M):
+            if not m.group(0).lstrip().startswith("typedef") and not m.group(1).endswith("_t"):
+                names.add(m.group(1))
+    return names
+
+
+def test_library_loads_and_exports_everything():
+    lib = vc.lib()
+    declared = _declared_functions()
+    assert declared, "header parse found nothing"
+    missing = [n for n in sorted(declared) if not hasattr(lib, n)]
+    assert not missing, f"declared but not exported: {missing}"
+    assert set(vc.EXPORTS) >= declared
+    assert lib.val_gpu_abi_version() == 1
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_struct_layout_matches_reference(golden):
+    src = r"""
+    #include "val_protocol.h"
+    #include "val_wire.h"
+    #include "val_crc32_gpu.h"
+    #include <stdio.h>
+    int main(void) {
+        val_config_t cfg = {0};
+        cfg.crc32_provider = val_gpu_crc32_provider;  /* the drop-in */
+        (void)cfg;
+        printf("%zu %zu %zu %zu\n", sizeof(val_config_t), offsetof(val_config_t, crc32_provider),
+               sizeof(val_packet_record_t), offsetof(val_config_t, buffers));
+        return 0;
+    }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        libdir = os.path.dirname(vc.LIB_PATH)
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{INC}", c, "-o", exe, f"-L{libdir}",
+                        "-l:libval_crc_hip.so", f"-Wl,-rpath,{libdir}", "-Wl,--unresolved-symbols=ignore-in-shared-libs"],
+                       check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    abi = golden["abi"]
+    assert [int(x) for x in out] == [abi["sizeof_val_config_t"], abi["offsetof_crc32_provider"],
+                                     abi["sizeof_val_packet_record_t"], abi["offsetof_buffers"]]
+
+
+def test_no_gpu_means_loud_failure_not_fallback():
+    if vc.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(vc.ValError) as e:
+        vc.init(0)
+    assert e.value.status == vc.VAL_ERR_IO

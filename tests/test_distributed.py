@@ -1,0 +1,61 @@
+"""World-size-2 gloo run of the sharding logic used by bench.py --gpus N:
+frames split by bytes with no overlap/gap, and a long window split into byte
+ranges whose partial states fold (product GF(2) shift) to the oracle CRC."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from val_protocol_amd.shard import fold_partials, shard_frames, shard_region
+
+
+def test_shard_frames_partition():
+    for n, w in [(0, 2), (1, 2), (7, 3), (1048576, 8), (131113, 8)]:
+        spans = [shard_frames(n, w, r) for r in range(w)]
+        assert spans[0][0] == 0 and sum(c for _, c in spans) == n
+        for (s0, c0), (s1, _) in zip(spans, spans[1:]):
+            assert s0 + c0 == s1
+    lens = np.random.default_rng(3).integers(520, 65532, 1000).astype(np.uint64)
+    spans = [shard_frames(1000, 4, r, lens) for r in range(4)]
+    assert sum(c for _, c in spans) == 1000
+    per = [int(lens[s:s + c].sum()) for s, c in spans]
+    assert max(per) - min(per) <= 2 * 65532
+
+
+def _worker(rank, world, port, data, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests import _oracle
+    import val_protocol_amd.crc as vc
+
+    start, cnt = shard_region(data.size, world, rank, align=64)
+    st = _oracle.update_state(0xFFFFFFFF if rank == 0 else 0, data[start:start + cnt])
+    t = torch.tensor([st, cnt], dtype=torch.int64)
+    out = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(out, t)  # host-side metadata only (2 words per rank)
+    if rank == 0:
+        parts = [(int(o[0]), int(o[1])) for o in out]
+        q.put(fold_partials(parts, vc.crc32_shift) ^ 0xFFFFFFFF)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_region_split_fold_gloo(world):
+    from tests import _oracle, _prng
+
+    data = _prng.prng_bytes(0xD15, 1_000_003)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 2000)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == _oracle.crc32(data)

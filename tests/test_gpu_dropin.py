@@ -1,0 +1,58 @@
+"""Drop-in witness: the reference protocol code (oracle/_ref/provider_harness,
+compiled from /root/reference/src) running with val_gpu_crc32_provider
+installed in val_config_t.crc32_provider -- TX framing, RX verify and a full
+1 MiB loopback transfer (BASELINE configs[0]) -- bit-identical to the same
+code running its built-in CRC."""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "provider_harness")
+LIB = os.path.join(ROOT, "val_protocol_amd", "libval_crc_hip.so")
+
+
+def _run(*args):
+    if not os.path.exists(HARNESS):
+        pytest.skip("provider_harness not built (needs the reference tree at build time)")
+    p = subprocess.run([HARNESS, *args], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    return [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def test_tx_trailers_from_gpu_provider():
+    rows = _run(LIB, "tx")
+    frames = [r for r in rows if r["mode"] == "tx"]
+    assert len(frames) == 20
+    for r in frames:
+        assert r["rc"] == 0
+        assert int.from_bytes(bytes.fromhex(r["trailer"]), "little") == r["ref_crc"], r
+    summary = [r for r in rows if r["mode"] == "tx_summary"][0]
+    assert summary["provider_calls"] == 20  # every trailer came from the GPU hook
+
+
+def test_rx_verify_with_gpu_provider():
+    rows = [r for r in _run(LIB, "rx") if r["mode"] == "rx"]
+    errs = 0
+    for r in rows:
+        if r["corrupt"] == 0:
+            assert r["rc"] == 0 and r["payload_ok"] == 1, r
+        else:
+            errs += 1
+            assert r["rc"] == -6, r  # VAL_ERR_CRC (src/val_core.c:965-974)
+        assert r["crc_errors"] == errs
+
+
+def test_loopback_1mib_gpu_equals_cpu():
+    cpu = _run("none", "loopback", "1048576", "1024")[0]
+    gpu = _run(LIB, "loopback", "1048576", "1024")[0]
+    for r in (cpu, gpu):
+        assert r["tx_status"] == 0 and r["rx_status"] == 0 and r["equal"] == 1, r
+        assert r["tx_crc_errors"] == 0 and r["rx_crc_errors"] == 0, r
+    assert gpu["provider_calls"] >= 2 * 1045  # every DATA frame hashed on TX and RX by the GPU hook
+    if cpu["retransmits"] == 0 and gpu["retransmits"] == 0:
+        assert gpu["tx_frames"] == cpu["tx_frames"] and gpu["tx_digest"] == cpu["tx_digest"]
+        assert gpu["rx_digest"] == cpu["rx_digest"]

@@ -1,0 +1,264 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference-derived golden vectors. Bit-exact everywhere (integer work)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import _oracle, _prng
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+GEOMS = [1, 2, 4, 8, 16, 32, 64]
+
+
+@pytest.fixture(scope="module")
+def vc():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import val_protocol_amd.crc as m
+
+    m.init(0)
+    yield m
+    m.set_lanes_per_frame(0)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda:0")
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+# ---- scalar hooks (host memory) ---------------------------------------------
+def test_kat(vc, golden):
+    assert vc.val_crc32(b"123456789") == 0xCBF43926 == golden["kat_123456789"]
+    assert vc.val_crc32(b"") == 0
+    assert vc.crc32_provider(0xFFFFFFFF, b"123456789") == 0xCBF43926
+
+
+def test_single_bytes(vc, golden):
+    assert [vc.val_crc32(bytes([b])) for b in range(256)] == golden["single_bytes"]
+
+
+def test_length_sweep(vc, golden):
+    data = _prng.prng_bytes(golden["sweep_seed"], 70000)
+    got = [vc.val_crc32(data[:L]) for L in range(0, 4097)]
+    assert got == golden["sweep_0_4096"]
+    for L, want in golden["sweep_special"].items():
+        assert vc.val_crc32(data[: int(L)]) == want
+
+
+def test_state_and_provider_semantics(vc, golden):
+    data = _prng.prng_bytes(golden["sweep_seed"], 70000)
+    for v in golden["state_vectors"]:
+        assert vc.val_crc32_update_state(v["seed"], data[: v["len"]]) == v["state"]
+        assert vc.crc32_provider(v["seed"], data[: v["len"]]) == v["final"]
+
+
+def test_regions_host(vc, golden):
+    data = _prng.prng_bytes(golden["region_seed"], 8 << 20)
+    for r in golden["regions"]:
+        L, c = r["len"], r["chunk"]
+        st = vc.val_crc32_init_state()
+        for o in range(0, L, c):
+            st = vc.val_crc32_update_state(st, data[o:min(L, o + c)])
+        assert vc.val_crc32_finalize_state(st) == r["crc"]
+        assert vc.val_crc32(data[:L]) == r["oneshot"]
+
+
+# ---- region (device) ---------------------------------------------------------
+@pytest.mark.parametrize("L", [0, 1, 2, 3, 4, 5, 7, 8, 63, 64, 65, 127, 128, 4095, 4096, 4097, 65535, 65536,
+                               65537, 1_000_003, (64 << 20) + 7])
+def test_region_dev(vc, dev, L):
+    data = _prng.prng_bytes(0xAB00 + L % 977, L)
+    d = torch.from_numpy(data).to(dev)
+    for state_in in (0xFFFFFFFF, 0, 0x1234ABCD):
+        out = vc.region(d, state_in)
+        torch.cuda.synchronize()
+        assert int(_u32(out)[0]) == _oracle.update_state(state_in, data)
+
+
+def test_region_256mib_window(vc, dev):
+    # Largest resume tail-verify window (reference src/val_receiver.c:161).
+    L = 256 << 20
+    data = _prng.prng_bytes(0x256, L)
+    d = torch.from_numpy(data).to(dev)
+    out = vc.region(d, 0xFFFFFFFF)
+    torch.cuda.synchronize()
+    assert int(_u32(out)[0]) ^ 0xFFFFFFFF == _oracle.crc32(data)
+
+
+# ---- batch frames ----------------------------------------------------------
+@pytest.mark.parametrize("G", GEOMS)
+@pytest.mark.parametrize("payload,explicit", [(1024, True), (1004, True), (16384, True), (400, False), (65516, True)])
+def test_frames_strided(vc, dev, G, payload, explicit):
+    n = 96 if payload > 20000 else 600
+    stream = _prng.frames_stream(n, payload, stride_pad=3, seed=0x51 ^ payload, explicit=explicit)
+    flen = 8 + payload + (8 if explicit else 0)
+    stride = flen + 4 + 3
+    vc.set_lanes_per_frame(G)
+    d = torch.from_numpy(stream).to(dev)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n, dtype=torch.int32, device=dev)
+    vc.frames(d, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+    torch.cuda.synchronize()
+    want, want_h = _oracle.frames_strided(stream, stride, flen, n, header=True)
+    assert np.array_equal(_u32(crc), want)
+    assert np.array_equal(_u32(hdr), want_h)
+
+
+def _ragged(seed, n, lo, hi):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    gaps = rng.integers(0, 7, n)  # byte-unaligned starts
+    offs = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        offs[i] = pos
+        pos += int(lens[i]) + 4
+    base = _prng.prng_bytes(seed, pos + 16)
+    return base, offs, lens
+
+
+@pytest.mark.parametrize("G", GEOMS)
+def test_frames_ragged_descriptors(vc, dev, G):
+    base, offs, lens = _ragged(100 + G, 700, 0, 70000)
+    lens[:40] = np.arange(40)  # tiny frames incl. 0..3 (byte path) and 4..39
+    vc.set_lanes_per_frame(G)
+    d = torch.from_numpy(base).to(dev)
+    do = torch.from_numpy(offs.view(np.int64)).to(dev)
+    dl = torch.from_numpy(lens.view(np.int32)).to(dev)
+    crc = torch.empty(offs.size, dtype=torch.int32, device=dev)
+    hdr = torch.empty(offs.size, dtype=torch.int32, device=dev)
+    vc.frames(d, off=do, length=dl, out_crc=crc, out_hdr=hdr)
+    torch.cuda.synchronize()
+    want, want_h = _oracle.frames(base, offs, lens, header=True)
+    assert np.array_equal(_u32(crc), want)
+    assert np.array_equal(_u32(hdr), want_h)
+
+
+@pytest.mark.parametrize("G", GEOMS)
+def test_every_length_0_to_600(vc, dev, G):
+    lens = np.arange(601, dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 5)]).astype(np.uint64)
+    base = _prng.prng_bytes(77, int(offs[-1]) + 700)
+    vc.set_lanes_per_frame(G)
+    d = torch.from_numpy(base).to(dev)
+    crc = vc.frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
+                    length=torch.from_numpy(lens.view(np.int32)).to(dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(crc), _oracle.frames(base, offs, lens))
+
+
+def _with_trailers(base, offs, lens):
+    crc = _oracle.frames(base, offs, lens)
+    for o, l, c in zip(offs, lens, crc):
+        base[int(o) + int(l):int(o) + int(l) + 4] = np.frombuffer(int(c).to_bytes(4, "little"), np.uint8)
+    return base
+
+
+@pytest.mark.parametrize("G", [1, 8, 64])
+def test_verify_detects_corruption(vc, dev, G):
+    base, offs, lens = _ragged(900 + G, 500, 8, 20000)
+    base = _with_trailers(base, offs, lens)
+    rng = np.random.default_rng(G)
+    bad = rng.choice(500, 23, replace=False)
+    for k, i in enumerate(bad):
+        o, l = int(offs[i]), int(lens[i])
+        pos = o + l + 3 if k % 3 == 0 else o + int(rng.integers(0, l))  # trailer byte or payload/header bit
+        base[pos] ^= np.uint8(1 << (k % 8))
+    want_ok, want_bad = _oracle.verify_frames(base, offs, lens)
+    assert want_bad == 23
+    vc.set_lanes_per_frame(G)
+    d = torch.from_numpy(base).to(dev)
+    ok, nbad = vc.verify_frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
+                                length=torch.from_numpy(lens.view(np.int32)).to(dev))
+    torch.cuda.synchronize()
+    assert int(nbad.item()) == 23
+    assert np.array_equal(ok.cpu().numpy(), want_ok)
+
+
+def test_reference_tx_frames_verify_on_gpu(vc, dev, golden):
+    # Frames produced by the reference TX path (golden, full wire bytes).
+    frames = [bytes.fromhex(f["wire"]) for f in golden["frames"] if "wire" in f]
+    offs, lens, blob = [], [], b""
+    for w in frames:
+        offs.append(len(blob))
+        lens.append(len(w) - 4)
+        blob += w
+    base = np.frombuffer(blob, np.uint8).copy()
+    ok, nbad = vc.verify_frames(torch.from_numpy(base).to(dev),
+                                off=torch.tensor(offs, dtype=torch.int64, device=dev),
+                                length=torch.tensor(lens, dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    assert int(nbad.item()) == 0 and bool(ok.all())
+
+
+def test_host_batch_api(vc):
+    vc.set_lanes_per_frame(0)
+    base, offs, lens = _ragged(31, 300, 0, 40000)
+    crc, hdr = vc.frames_host(base, offs, lens, header=True)
+    want, want_h = _oracle.frames(base, offs, lens, header=True)
+    assert np.array_equal(crc, want) and np.array_equal(hdr, want_h)
+    base = _with_trailers(base, offs, lens)
+    st, ok, nbad = vc.verify_frames_host(base, offs, lens)
+    assert st == vc.VAL_OK and nbad == 0 and ok.all()
+    base[int(offs[5]) + 1] ^= 0x10
+    st, ok, nbad = vc.verify_frames_host(base, offs, lens)
+    assert st == vc.VAL_ERR_CRC and nbad == 1 and ok[5] == 0
+    with pytest.raises(vc.ValError) as e:  # frame overruns the buffer
+        vc.frames_host(base[:100], np.array([90], np.uint64), np.array([20], np.uint32))
+    assert e.value.status == vc.VAL_ERR_INVALID_ARG
+
+
+def test_cfg3_full_size_properties(vc, dev):
+    """1 M x 16 KiB explicit-offset DATA frames (BASELINE cfg3, 17.2 GB).
+    Size-independent checks: trailer write -> verify round trip has zero
+    mismatches, exactly the corrupted frames fail, and a random sample of
+    frames is bit-exact against the oracle."""
+    vc.set_lanes_per_frame(0)
+    n, payload = 1 << 20, 16384
+    flen, stride = 8 + 8 + payload, 8 + 8 + payload + 4
+    g = torch.Generator(device=dev).manual_seed(3)
+    buf = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device=dev, generator=g)
+    buf[:, 0], buf[:, 1], buf[:, 2], buf[:, 3] = 5, 1, (payload + 8) & 0xFF, (payload + 8) >> 8
+    buf[:, 4:8] = 0
+    offs = torch.arange(n, device=dev, dtype=torch.int64) * payload
+    buf[:, 8:16] = offs.view(torch.uint8).view(n, 8)
+    flat = buf.view(-1)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n, dtype=torch.int32, device=dev)
+    vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+    buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
+    ok, nbad = vc.verify_frames(flat, stride=stride, flen=flen, n=n)
+    torch.cuda.synchronize()
+    assert int(nbad.item()) == 0 and bool(ok.all())
+    hot = [0, 1, n // 2, n - 1]
+    for i in hot[:3]:
+        buf[i, 100 + i % 7] ^= 0x01
+    ok, nbad = vc.verify_frames(flat, stride=stride, flen=flen, n=n)
+    torch.cuda.synchronize()
+    assert int(nbad.item()) == 3
+    bad_idx = torch.nonzero(ok == 0).flatten().cpu().tolist()
+    assert bad_idx == hot[:3]
+    for i in hot[:3]:
+        buf[i, 100 + i % 7] ^= 0x01
+    rng = np.random.default_rng(5)
+    sample = np.unique(np.concatenate([rng.choice(n, 1500, replace=False), hot]))
+    rows = buf[torch.from_numpy(sample).to(dev)].cpu().numpy().reshape(-1)
+    want, want_h = _oracle.frames_strided(rows, stride, flen, sample.size, header=True)
+    assert np.array_equal(_u32(crc)[sample], want)
+    assert np.array_equal(_u32(hdr)[sample], want_h)
+    h0 = _u32(hdr)
+    assert np.all(h0 == h0[0])  # every header is identical in this stream
+
+
+def test_no_cpu_fallback_symbols_loaded(vc):
+    # The product library must be the one mapped in this process.
+    maps = open("/proc/self/maps").read()
+    assert os.path.basename(vc.LIB_PATH) in maps

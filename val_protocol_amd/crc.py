@@ -1,0 +1,287 @@
+"""Python host binding of the MI355X CRC-32 integrity path.
+
+Thin ctypes layer over ``val_protocol_amd/libval_crc_hip.so`` (C ABI declared
+in ``include/val_crc32_gpu.h``). Names mirror the reference interface:
+
+* ``val_crc32`` / ``val_crc32_init_state`` / ``val_crc32_update_state`` /
+  ``val_crc32_finalize_state`` -- reference ``src/val_core.c:150-183``
+* ``crc32_provider`` -- a ``crc32_func_t`` (reference
+  ``include/val_protocol.h:163-166``); ``provider_address()`` returns the C
+  function pointer to install into ``val_config_t.crc32_provider``
+* ``frames`` / ``verify_frames`` -- batched trailer CRC / RX verify of DATA
+  frames (reference ``src/val_core.c:828-834`` and ``:963-974``)
+* ``region`` -- long-window CRC (reference ``src/val_core.c:414-455``)
+
+Every call computes on the GPU. If the shared library is missing or the GPU
+path fails, calls raise; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+VAL_OK = 0
+VAL_ERR_INVALID_ARG = -1
+VAL_ERR_NO_MEMORY = -2
+VAL_ERR_IO = -3
+VAL_ERR_CRC = -6
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libval_crc_hip.so")
+
+# Exported symbols (kept in sync with include/*.h; tests/test_abi.py checks).
+EXPORTS = (
+    "val_gpu_init", "val_gpu_shutdown", "val_gpu_device_count", "val_gpu_abi_version",
+    "val_gpu_last_error", "val_gpu_lanes_per_frame", "val_gpu_set_lanes_per_frame",
+    "val_gpu_crc32_provider", "val_crc32_combine", "val_crc32_shift",
+    "val_crc32", "val_crc32_init_state", "val_crc32_update_state", "val_crc32_finalize_state",
+    "val_crc32_frames_dev", "val_crc32_verify_frames_dev", "val_crc32_region_dev",
+    "val_crc32_region_scratch_bytes", "val_crc32_frames_host", "val_crc32_verify_frames_host",
+    "val_serialize_frame_header", "val_deserialize_frame_header", "val_frame_data_batch",
+    "val_frame_put_trailers", "val_frame_scan",
+)
+
+
+class ValError(RuntimeError):
+    def __init__(self, status: int, where: str, detail: str = ""):
+        super().__init__(f"{where} failed: status {status} {detail}".strip())
+        self.status = status
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    def fn(name, res, *args):
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = list(args)
+
+    i32, u32, u64, sz = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+    fn("val_gpu_init", i32, ctypes.c_int)
+    fn("val_gpu_shutdown", None)
+    fn("val_gpu_device_count", ctypes.c_int)
+    fn("val_gpu_abi_version", u32)
+    fn("val_gpu_last_error", ctypes.c_char_p)
+    fn("val_gpu_lanes_per_frame", u32, u32)
+    fn("val_gpu_set_lanes_per_frame", i32, u32)
+    fn("val_gpu_crc32_provider", u32, u32, _vp, sz)
+    fn("val_crc32_combine", u32, u32, u32, u64)
+    fn("val_crc32_shift", u32, u32, u64)
+    fn("val_crc32", u32, _vp, sz)
+    fn("val_crc32_init_state", u32)
+    fn("val_crc32_update_state", u32, u32, _vp, sz)
+    fn("val_crc32_finalize_state", u32, u32)
+    fn("val_crc32_frames_dev", i32, _vp, _vp, _vp, u64, u32, u32, u32, _vp, _vp, _vp)
+    fn("val_crc32_verify_frames_dev", i32, _vp, _vp, _vp, u64, u32, u32, u32, _vp, _vp, _vp, _vp, _vp)
+    fn("val_crc32_region_dev", i32, _vp, u64, u32, _vp, _vp)
+    fn("val_crc32_region_scratch_bytes", u64, u64)
+    fn("val_crc32_frames_host", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp)
+    fn("val_crc32_verify_frames_host", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp)
+    fn("val_serialize_frame_header", None, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16, u32, _vp)
+    fn("val_deserialize_frame_header", None, _vp, _vp, _vp, _vp, _vp)
+    fn("val_frame_data_batch", i32, _vp, _vp, _vp, _vp, _vp, u32, _vp, sz, _vp, _vp, ctypes.POINTER(sz))
+    fn("val_frame_put_trailers", None, _vp, _vp, _vp, _vp, u32)
+    fn("val_frame_scan", i32, _vp, sz, sz, u32, _vp, _vp, ctypes.POINTER(u32), ctypes.POINTER(sz))
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP shared library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() first (no CPU fallback)")
+        try:  # one HIP runtime per process: let torch's libamdhip64 load first
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is always present in this image
+            pass
+        l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        _declare(l)
+        _lib = l
+    return _lib
+
+
+def last_error() -> str:
+    return lib().val_gpu_last_error().decode(errors="replace")
+
+
+def _check(st: int, where: str) -> None:
+    if st != VAL_OK:
+        raise ValError(st, where, last_error())
+
+
+def _buf(data) -> tuple[ctypes.c_void_p, int, object]:
+    """Host byte buffer -> (pointer, length, keepalive)."""
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(bytes(data) if isinstance(data, memoryview) else data, dtype=np.uint8)
+    else:
+        arr = np.ascontiguousarray(np.asarray(data).view(np.uint8).reshape(-1))
+    return ctypes.c_void_p(arr.ctypes.data if arr.size else 0), int(arr.size), arr
+
+
+# ---- scalar surface -------------------------------------------------------
+def init(device: int = 0) -> None:
+    _check(lib().val_gpu_init(device), "val_gpu_init")
+
+
+def device_count() -> int:
+    return int(lib().val_gpu_device_count())
+
+
+def val_crc32(data) -> int:
+    p, n, keep = _buf(data)
+    return int(lib().val_crc32(p, n))
+
+
+def val_crc32_init_state() -> int:
+    return int(lib().val_crc32_init_state())
+
+
+def val_crc32_update_state(state: int, data) -> int:
+    p, n, keep = _buf(data)
+    return int(lib().val_crc32_update_state(state & 0xFFFFFFFF, p, n))
+
+
+def val_crc32_finalize_state(state: int) -> int:
+    return int(lib().val_crc32_finalize_state(state & 0xFFFFFFFF))
+
+
+def crc32_provider(seed: int, data) -> int:
+    p, n, keep = _buf(data)
+    return int(lib().val_gpu_crc32_provider(seed & 0xFFFFFFFF, p, n))
+
+
+def provider_address() -> int:
+    """Address of the C function to store in val_config_t.crc32_provider."""
+    return ctypes.cast(lib().val_gpu_crc32_provider, ctypes.c_void_p).value
+
+
+def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return int(lib().val_crc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b))
+
+
+def crc32_shift(state: int, nbytes: int) -> int:
+    return int(lib().val_crc32_shift(state & 0xFFFFFFFF, nbytes))
+
+
+def lanes_per_frame(typical_len: int) -> int:
+    return int(lib().val_gpu_lanes_per_frame(typical_len))
+
+
+def set_lanes_per_frame(lanes: int) -> None:
+    """Force the lanes-per-frame geometry (0 = automatic). Speed only."""
+    _check(lib().val_gpu_set_lanes_per_frame(lanes), "val_gpu_set_lanes_per_frame")
+
+
+# ---- device-resident batches (torch tensors on the GPU) ---------------------
+def _dptr(t) -> ctypes.c_void_p:
+    if t is None:
+        return ctypes.c_void_p(0)
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError("device call needs contiguous GPU tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_ptr(stream) -> ctypes.c_void_p:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def frames(base, *, off=None, length=None, stride: int = 0, flen: int = 0, n: Optional[int] = None,
+           out_crc=None, out_hdr=None, len_hint: int = 0, stream=None):
+    """Trailer CRC (and optional header_crc) of every frame, device-resident.
+
+    ``base``: uint8 GPU tensor. Descriptor mode: ``off`` (int64) and
+    ``length`` (int32) GPU tensors. Strided mode: ``stride``/``flen``/``n``.
+    Outputs are int32 GPU tensors holding the uint32 bit patterns.
+    Launches on torch's current stream (or ``stream``) and returns at once.
+    """
+    import torch
+
+    if n is None:
+        n = int(off.numel()) if off is not None else 0
+    if out_crc is None:
+        out_crc = torch.empty(n, dtype=torch.int32, device=base.device)
+    st = lib().val_crc32_frames_dev(_dptr(base), _dptr(off), _dptr(length), stride, flen, n, len_hint,
+                                    _dptr(out_crc), _dptr(out_hdr), _stream_ptr(stream))
+    _check(st, "val_crc32_frames_dev")
+    return out_crc
+
+
+def verify_frames(base, *, off=None, length=None, stride: int = 0, flen: int = 0, n: Optional[int] = None,
+                  out_ok=None, nbad=None, out_crc=None, out_hdr=None, len_hint: int = 0, stream=None):
+    """RX batch verify. Returns (ok uint8 tensor, nbad int32[1] tensor)."""
+    import torch
+
+    if n is None:
+        n = int(off.numel()) if off is not None else 0
+    dev = base.device
+    if out_ok is None:
+        out_ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    if nbad is None:
+        nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = lib().val_crc32_verify_frames_dev(_dptr(base), _dptr(off), _dptr(length), stride, flen, n, len_hint,
+                                           _dptr(out_ok), _dptr(nbad), _dptr(out_crc), _dptr(out_hdr),
+                                           _stream_ptr(stream))
+    _check(st, "val_crc32_verify_frames_dev")
+    return out_ok, nbad
+
+
+def region(buf, state_in: int = 0xFFFFFFFF, out=None, stream=None):
+    """Raw register after feeding the whole uint8 GPU tensor ``buf``."""
+    import torch
+
+    if out is None:
+        out = torch.empty(1, dtype=torch.int32, device=buf.device)
+    st = lib().val_crc32_region_dev(_dptr(buf), int(buf.numel()), state_in & 0xFFFFFFFF, _dptr(out),
+                                    _stream_ptr(stream))
+    _check(st, "val_crc32_region_dev")
+    return out
+
+
+# ---- host-memory batches ----------------------------------------------------
+def frames_host(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
+                stride: int = 0, flen: int = 0, n: Optional[int] = None, header: bool = False):
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.size
+    crc = np.zeros(n, dtype=np.uint32)
+    hdr = np.zeros(n, dtype=np.uint32) if header else None
+    st = lib().val_crc32_frames_host(base.ctypes.data, base.size,
+                                     off.ctypes.data if off is not None else None,
+                                     length.ctypes.data if length is not None else None,
+                                     stride, flen, n, crc.ctypes.data,
+                                     hdr.ctypes.data if hdr is not None else None)
+    _check(st, "val_crc32_frames_host")
+    return (crc, hdr) if header else crc
+
+
+def verify_frames_host(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
+                       stride: int = 0, flen: int = 0, n: Optional[int] = None):
+    """Returns (status, ok uint8 array, nbad). status VAL_ERR_CRC on mismatch."""
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.size
+    ok = np.zeros(n, dtype=np.uint8)
+    nbad = ctypes.c_uint32(0)
+    st = lib().val_crc32_verify_frames_host(base.ctypes.data, base.size,
+                                            off.ctypes.data if off is not None else None,
+                                            length.ctypes.data if length is not None else None,
+                                            stride, flen, n, ok.ctypes.data, ctypes.byref(nbad))
+    if st not in (VAL_OK, VAL_ERR_CRC):
+        _check(st, "val_crc32_verify_frames_host")
+    return st, ok, int(nbad.value)

@@ -1,0 +1,123 @@
+/*
+ * val_wire.c -- host-side frame codec and batch framing for the MI355X CRC
+ * path (C99). The GPU kernels hash what these helpers lay out.
+ *
+ * Header codec: same byte layout as the reference (src/val_wire.c:27-45).
+ * Batch framing: the per-frame body of val__internal_send_packet_core
+ * (src/val_core.c:733-832) applied to a whole window of DATA frames at once,
+ * so one kernel launch can fill every trailer.
+ * Stream scan: the header/length checks of val_internal_recv_packet
+ * (src/val_core.c:893-921) applied to a buffered byte stream (8(f) f2).
+ */
+#include <string.h>
+
+#include "val_byte_order.h"
+#include "val_wire.h"
+
+void val_serialize_frame_header(uint8_t type, uint8_t flags, uint16_t content_len, uint32_t type_data, uint8_t *wiredata)
+{
+    if (!wiredata)
+        return;
+    wiredata[0] = type;
+    wiredata[1] = flags;
+    val_put_le16(wiredata + 2, content_len);
+    val_put_le32(wiredata + 4, type_data);
+}
+
+void val_deserialize_frame_header(const uint8_t *wiredata, uint8_t *type, uint8_t *flags, uint16_t *content_len,
+                                  uint32_t *type_data)
+{
+    if (!wiredata)
+        return;
+    if (type)
+        *type = wiredata[0];
+    if (flags)
+        *flags = wiredata[1];
+    if (content_len)
+        *content_len = val_get_le16(wiredata + 2);
+    if (type_data)
+        *type_data = val_get_le32(wiredata + 4);
+}
+
+val_status_t val_frame_data_batch(const uint8_t *payload, const uint64_t *pay_off, const uint32_t *pay_len,
+                                  const uint64_t *file_off, const uint8_t *include_offset, uint32_t n, uint8_t *out,
+                                  size_t out_cap, uint64_t *frame_off, uint32_t *crc_len, size_t *out_used)
+{
+    if (out_used)
+        *out_used = 0;
+    if (n && (!pay_len || !file_off || !out || !frame_off || !crc_len))
+        return VAL_ERR_INVALID_ARG;
+    size_t pos = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const int explicit_off = include_offset ? (include_offset[i] != 0) : 1;
+        const uint64_t content = (uint64_t)pay_len[i] + (explicit_off ? 8u : 0u);
+        if (content > VAL_WIRE_MAX_CONTENT)
+            return VAL_ERR_INVALID_ARG; /* the reference would wrap content_len here */
+        if (pay_len[i] && (!payload || !pay_off))
+            return VAL_ERR_INVALID_ARG;
+        const size_t wire = VAL_WIRE_HEADER_SIZE + (size_t)content + VAL_WIRE_TRAILER_SIZE;
+        if (wire > out_cap - pos)
+            return VAL_ERR_INVALID_ARG;
+        uint8_t *f = out + pos;
+        val_serialize_frame_header((uint8_t)VAL_PKT_DATA, explicit_off ? (uint8_t)VAL_DATA_OFFSET_PRESENT : 0u,
+                                   (uint16_t)content, 0u, f);
+        uint8_t *c = f + VAL_WIRE_HEADER_SIZE;
+        if (explicit_off) {
+            val_put_le64(c, file_off[i]);
+            c += 8;
+        }
+        if (pay_len[i])
+            memcpy(c, payload + pay_off[i], pay_len[i]);
+        memset(f + VAL_WIRE_HEADER_SIZE + content, 0, VAL_WIRE_TRAILER_SIZE);
+        frame_off[i] = pos;
+        crc_len[i] = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
+        pos += wire;
+    }
+    if (out_used)
+        *out_used = pos;
+    return VAL_OK;
+}
+
+void val_frame_put_trailers(uint8_t *stream, const uint64_t *frame_off, const uint32_t *crc_len, const uint32_t *crc,
+                            uint32_t n)
+{
+    for (uint32_t i = 0; i < n; i++)
+        val_put_le32(stream + frame_off[i] + crc_len[i], crc[i]);
+}
+
+val_status_t val_frame_scan(const uint8_t *stream, size_t len, size_t mtu, uint32_t max_frames, uint64_t *frame_off,
+                            uint32_t *crc_len, uint32_t *n_frames, size_t *consumed)
+{
+    if (n_frames)
+        *n_frames = 0;
+    if (consumed)
+        *consumed = 0;
+    if ((!stream && len) || !frame_off || !crc_len)
+        return VAL_ERR_INVALID_ARG;
+    if (mtu < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE)
+        return VAL_ERR_INVALID_ARG;
+    const size_t max_content = mtu - VAL_WIRE_HEADER_SIZE - VAL_WIRE_TRAILER_SIZE;
+    size_t pos = 0;
+    uint32_t k = 0;
+    val_status_t st = VAL_OK;
+    while (k < max_frames && len - pos >= VAL_WIRE_HEADER_SIZE) {
+        uint16_t content = 0;
+        val_deserialize_frame_header(stream + pos, NULL, NULL, &content, NULL);
+        if ((size_t)content > max_content) {
+            st = VAL_ERR_PROTOCOL;
+            break;
+        }
+        const size_t wire = VAL_WIRE_HEADER_SIZE + (size_t)content + VAL_WIRE_TRAILER_SIZE;
+        if (len - pos < wire)
+            break; /* incomplete frame: wait for more bytes */
+        frame_off[k] = pos;
+        crc_len[k] = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
+        k++;
+        pos += wire;
+    }
+    if (n_frames)
+        *n_frames = k;
+    if (consumed)
+        *consumed = pos;
+    return st;
+}
