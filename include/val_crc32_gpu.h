@@ -1,7 +1,7 @@
 /*
  * val_crc32_gpu.h -- C ABI of the MI355X (gfx950) CRC-32 integrity path.
  * Exported by val_protocol_amd/libval_crc_hip.so. Plain C types only; HIP
- * streams travel as `void *` (a hipStream_t, NULL = the library's stream).
+ * streams travel as `void *` (a hipStream_t; NULL = the HIP default stream).
  *
  * What each entry point replaces in the reference (VAL v0.7):
  *   val_gpu_crc32_provider  -> a crc32_func_t for val_config_t.crc32_provider

@@ -202,7 +202,9 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
                     const u32x4u v1 = *reinterpret_cast<const u32x4u *>(up + 16);
                     const u32x4u v2 = *reinterpret_cast<const u32x4u *>(up + 32);
                     const u32x4u v3 = *reinterpret_cast<const u32x4u *>(up + 48);
-                    acc = s4_step(acc, v0.x, sb); acc = s4_step(acc, v0.y, sb);
+                    // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
+                    const uint32_t w0 = (u == 1 && pad > kUnit - 4) ? v0.x ^ (seed >> (8 * (kUnit - pad))) : v0.x;
+                    acc = s4_step(acc, w0, sb); acc = s4_step(acc, v0.y, sb);
                     acc = s4_step(acc, v0.z, sb); acc = s4_step(acc, v0.w, sb);
                     acc = s4_step(acc, v1.x, sb); acc = s4_step(acc, v1.y, sb);
                     acc = s4_step(acc, v1.z, sb); acc = s4_step(acc, v1.w, sb);
@@ -413,7 +415,8 @@ val_status_t launch_frames(FrameParams &p, uint32_t G, hipStream_t s)
     return VAL_OK;
 }
 
-hipStream_t pick_stream(void *stream) { return stream ? (hipStream_t)stream : g_ctx.stream; }
+// NULL selects the HIP default (null) stream, as in every HIP API.
+hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 
 // Chunking of a long region into "frames" for stage 1.
 void region_geometry(uint64_t len, uint64_t *clen, uint32_t *nchunks)
