@@ -105,6 +105,13 @@ uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);
  * process; 0 restores the automatic choice. Returns VAL_ERR_INVALID_ARG for
  * other values. Results never depend on it; only speed does. */
 val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
+/* Independent CRC chains each lane runs (1 or 2; 0 = automatic). */
+uint32_t val_gpu_chains_per_lane(uint32_t typical_len);
+val_status_t val_gpu_set_chains_per_lane(uint32_t chains);
+/* Bytes a lane hashes per round (64 or 128; 0 = automatic). */
+val_status_t val_gpu_set_unit_bytes(uint32_t unit);
+/* Register prefetch of the next round (1 on, 0 off, -1 automatic). */
+val_status_t val_gpu_set_prefetch(int on);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 GEOMS = [1, 2, 4, 8, 16, 32, 64]
+# (chains per lane, unit bytes, prefetch) variants of the frames kernel
+VARIANTS = [(1, 64, 0), (1, 64, 1), (1, 128, 0), (1, 128, 1), (2, 64, 0)]
 
 
 @pytest.fixture(scope="module")
@@ -21,7 +23,7 @@ def vc():
 
     m.init(0)
     yield m
-    m.set_lanes_per_frame(0)
+    m.set_geometry()
 
 
 @pytest.fixture(scope="module")
@@ -100,7 +102,7 @@ def test_frames_strided(vc, dev, G, payload, explicit):
     stream = _prng.frames_stream(n, payload, stride_pad=3, seed=0x51 ^ payload, explicit=explicit)
     flen = 8 + payload + (8 if explicit else 0)
     stride = flen + 4 + 3
-    vc.set_lanes_per_frame(G)
+    vc.set_geometry(G, *VARIANTS[G % len(VARIANTS)])
     d = torch.from_numpy(stream).to(dev)
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n, dtype=torch.int32, device=dev)
@@ -125,11 +127,12 @@ def _ragged(seed, n, lo, hi):
     return base, offs, lens
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("G", GEOMS)
-def test_frames_ragged_descriptors(vc, dev, G):
+def test_frames_ragged_descriptors(vc, dev, G, variant):
     base, offs, lens = _ragged(100 + G, 700, 0, 70000)
     lens[:40] = np.arange(40)  # tiny frames incl. 0..3 (byte path) and 4..39
-    vc.set_lanes_per_frame(G)
+    vc.set_geometry(G, *variant)
     d = torch.from_numpy(base).to(dev)
     do = torch.from_numpy(offs.view(np.int64)).to(dev)
     dl = torch.from_numpy(lens.view(np.int32)).to(dev)
@@ -142,12 +145,13 @@ def test_frames_ragged_descriptors(vc, dev, G):
     assert np.array_equal(_u32(hdr), want_h)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("G", GEOMS)
-def test_every_length_0_to_600(vc, dev, G):
+def test_every_length_0_to_600(vc, dev, G, variant):
     lens = np.arange(601, dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 5)]).astype(np.uint64)
     base = _prng.prng_bytes(77, int(offs[-1]) + 700)
-    vc.set_lanes_per_frame(G)
+    vc.set_geometry(G, *variant)
     d = torch.from_numpy(base).to(dev)
     crc = vc.frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
                     length=torch.from_numpy(lens.view(np.int32)).to(dev))
@@ -174,7 +178,7 @@ def test_verify_detects_corruption(vc, dev, G):
         base[pos] ^= np.uint8(1 << (k % 8))
     want_ok, want_bad = _oracle.verify_frames(base, offs, lens)
     assert want_bad == 23
-    vc.set_lanes_per_frame(G)
+    vc.set_geometry(G, *VARIANTS[G % len(VARIANTS)])
     d = torch.from_numpy(base).to(dev)
     ok, nbad = vc.verify_frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
                                 length=torch.from_numpy(lens.view(np.int32)).to(dev))
@@ -200,7 +204,7 @@ def test_reference_tx_frames_verify_on_gpu(vc, dev, golden):
 
 
 def test_host_batch_api(vc):
-    vc.set_lanes_per_frame(0)
+    vc.set_geometry()
     base, offs, lens = _ragged(31, 300, 0, 40000)
     crc, hdr = vc.frames_host(base, offs, lens, header=True)
     want, want_h = _oracle.frames(base, offs, lens, header=True)
@@ -221,7 +225,7 @@ def test_cfg3_full_size_properties(vc, dev):
     Size-independent checks: trailer write -> verify round trip has zero
     mismatches, exactly the corrupted frames fail, and a random sample of
     frames is bit-exact against the oracle."""
-    vc.set_lanes_per_frame(0)
+    vc.set_geometry()
     n, payload = 1 << 20, 16384
     flen, stride = 8 + 8 + payload, 8 + 8 + payload + 4
     g = torch.Generator(device=dev).manual_seed(3)

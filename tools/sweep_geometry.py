@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Times the frames kernel for every lanes-per-frame geometry on the BASELINE
-shapes (device-resident, HIP events on the launch stream). Diagnostic only."""
+"""Times the frames kernel for kernel geometries on the BASELINE shapes
+(device-resident, HIP events on the launch stream). Diagnostic only.
+
+SWEEP_COMBOS="G:CH:UNIT:PF,..." overrides the default list."""
 import os
 import sys
 
@@ -10,6 +12,12 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 import val_protocol_amd.crc as vc  # noqa: E402
+
+DEFAULT = {
+    "cfg3": [(g, c, u, p) for g in (4, 8, 16, 32) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (1, 128, 1), (2, 64, 0))],
+    "cfg4": [(g, c, u, p) for g in (8, 16, 32, 64) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (1, 128, 1), (2, 64, 0))],
+    "cfg2": [(g, c, u, p) for g in (1, 2, 4, 8) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (2, 64, 0))],
+}
 
 
 def time_it(fn, reps=10):
@@ -30,23 +38,26 @@ def time_it(fn, reps=10):
 def main():
     dev = torch.device("cuda:0")
     vc.init(0)
-    cfgs = sys.argv[1:] or ["cfg3", "cfg2", "cfg4"]
+    cfgs = sys.argv[1:] or ["cfg3", "cfg4", "cfg2"]
+    env = os.environ.get("SWEEP_COMBOS")
     for name in cfgs:
+        combos = [tuple(int(x) for x in c.split(":")) for c in env.split(",")] if env else DEFAULT[name]
         n, payload, explicit, header = bench.CONFIGS[name]
         buf, flen, stride = bench.make_frames(torch, dev, n, payload, explicit, 0, 7)
         flat = buf.view(-1)
         crc = torch.empty(n, dtype=torch.int32, device=dev)
         hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
-        ref = None
-        for G in [1, 2, 4, 8, 16, 32, 64]:
-            vc.set_lanes_per_frame(G)
+        vc.set_geometry()
+        vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+        ref = crc.clone()
+        for G, CH, U, PF in combos:
+            vc.set_geometry(G, CH, U, PF)
             med, best = time_it(lambda: vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr))
-            out = crc.clone()
-            same = True if ref is None else bool(torch.equal(out, ref))
-            ref = out if ref is None else ref
+            same = bool(torch.equal(crc, ref))
             gbs = n * flen / (med * 1e-3) / 1e9
-            print(f"{name} G={G:2d}: median {med:.3f} ms best {best:.3f} ms  {gbs:7.1f} GB/s  same={same}", flush=True)
-        vc.set_lanes_per_frame(0)
+            print(f"{name} G={G:2d} CH={CH} UNIT={U:3d} PF={PF}: median {med:.3f} ms best {best:.3f} ms "
+                  f"{gbs:7.1f} GB/s same={same}", flush=True)
+        vc.set_geometry()
         del buf, flat
         torch.cuda.empty_cache()
 

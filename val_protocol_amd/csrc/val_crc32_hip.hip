@@ -40,12 +40,11 @@
 
 namespace vcrc {
 
-constexpr int kUnit = 64;      // bytes a lane hashes per round
 constexpr int kBlock = 1024;   // threads per workgroup (16 waves)
 constexpr uint32_t kLdsS4 = 0;          // 2 table pairs x 256 rows x 256 B
 constexpr uint32_t kLdsGap = 131072;    // 8 nibble tables x 16 rows x 128 B
 constexpr uint32_t kLdsWords = (131072 + 16384) / 4;
-constexpr int kMaxTree = 6;    // log2(64)
+constexpr int kMaxTree = 7;    // log2(max virtual lanes = 128)
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t u32u __attribute__((aligned(1)));
@@ -158,11 +157,75 @@ __device__ void build_tables(const FrameParams &p)
     __syncthreads();
 }
 
+// Words of one virtual lane's unit for round 0 (see header comment):
+// u > 0: a full unit of unaligned dwordx4 loads; u == 0: the front-padded
+// first unit, assembled word by word with the seed XORed into frame bytes
+// 0..3; u < 0: nothing (zeros keep a zero register zero). Frames shorter than
+// 4 bytes take the byte path instead (tiny = true).
+template <int UNIT>
+__device__ __forceinline__ void load_unit(uint32_t (&w)[UNIT / 4], int u, const uint8_t *fp, uint32_t L, uint32_t pad,
+                                          uint32_t seed, bool &tiny)
+{
+    tiny = false;
+    if (u > 0) {
+        const uint8_t *up = fp + (uint64_t)u * UNIT - pad;
+#pragma unroll
+        for (int q = 0; q < UNIT / 16; q++) {
+            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
+            w[4 * q + 0] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+        // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
+        if (u == 1 && pad > UNIT - 4) w[0] ^= seed >> (8 * (UNIT - pad));
+    } else if (u == 0 && L >= 4) {
+#pragma unroll
+        for (int i = 0; i < UNIT / 4; i++) {
+            const int q = 4 * i - (int)pad;  // frame offset of this word
+            uint32_t x = 0;
+            if (q >= 0) {
+                x = ld32(fp + q);
+                if (q < 4) x ^= seed >> (8 * q);
+            } else if (q > -4) {
+                x = (ld32(fp) ^ seed) << (8 * (-q));
+            }
+            w[i] = x;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < UNIT / 4; i++) w[i] = 0;
+        tiny = (u == 0);
+    }
+}
+
+template <int CH, int G, int UNIT>
+__device__ __forceinline__ void load_round(uint32_t (&w)[CH][UNIT / 4], const uint8_t *up)
+{
+#pragma unroll
+    for (int c = 0; c < CH; c++) {
+#pragma unroll
+        for (int q = 0; q < UNIT / 16; q++) {
+            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + (uint64_t)G * UNIT * c + 16 * q);
+            w[c][4 * q + 0] = v.x;
+            w[c][4 * q + 1] = v.y;
+            w[c][4 * q + 2] = v.z;
+            w[c][4 * q + 3] = v.w;
+        }
+    }
+}
+
 // K1/K2/K3 fused: per-frame CRC (trailer), optional header_crc and verify.
-template <int G>
+// G lanes per frame, CH independent chains per lane -> V = G*CH virtual lanes;
+// virtual lane v = g + G*c owns units v, v+V, v+2V, ... (counted so virtual
+// lane V-1 owns the last unit). UNIT bytes per unit. PF: load the next
+// round's units before hashing the current one (register double buffer).
+template <int G, int CH, int UNIT, bool PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
-    build_tables<G>(p);
+    constexpr int V = G * CH;
+    constexpr int W = UNIT / 4;
+    build_tables<V>(p);
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const uint32_t lo4 = (uint32_t)(lane & 31) << 2;
@@ -188,63 +251,85 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         }
         const uint8_t *fp = p.base + off;
         const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
-        const uint32_t U = L ? (L + kUnit - 1) / kUnit : 1u;
-        const uint32_t R = (U + G - 1) / G;
-        const uint32_t pad = U * kUnit - L;
-        uint32_t acc = 0;
-        if (active) {
-            for (uint32_t k = 0; k < R; k++) {
-                const int u = (int)U - G * (int)(R - k) + g;
-                if (G > 1) acc = gap_step(acc, lo4);
-                if (u > 0) {
-                    const uint8_t *up = fp + (uint64_t)u * kUnit - pad;
-                    const u32x4u v0 = *reinterpret_cast<const u32x4u *>(up);
-                    const u32x4u v1 = *reinterpret_cast<const u32x4u *>(up + 16);
-                    const u32x4u v2 = *reinterpret_cast<const u32x4u *>(up + 32);
-                    const u32x4u v3 = *reinterpret_cast<const u32x4u *>(up + 48);
-                    // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
-                    const uint32_t w0 = (u == 1 && pad > kUnit - 4) ? v0.x ^ (seed >> (8 * (kUnit - pad))) : v0.x;
-                    acc = s4_step(acc, w0, sb); acc = s4_step(acc, v0.y, sb);
-                    acc = s4_step(acc, v0.z, sb); acc = s4_step(acc, v0.w, sb);
-                    acc = s4_step(acc, v1.x, sb); acc = s4_step(acc, v1.y, sb);
-                    acc = s4_step(acc, v1.z, sb); acc = s4_step(acc, v1.w, sb);
-                    acc = s4_step(acc, v2.x, sb); acc = s4_step(acc, v2.y, sb);
-                    acc = s4_step(acc, v2.z, sb); acc = s4_step(acc, v2.w, sb);
-                    acc = s4_step(acc, v3.x, sb); acc = s4_step(acc, v3.y, sb);
-                    acc = s4_step(acc, v3.z, sb); acc = s4_step(acc, v3.w, sb);
-                } else if (u == 0) {
-                    // First (front-padded) unit: only frame bytes [0, UNIT - pad) are real.
-                    if (L < 4) {
-                        uint32_t c = seed;
-                        for (uint32_t i = 0; i < L; i++) c = byte_step(c, fp[i], sb);
-                        acc = c;
-                    } else {
-                        for (int i = 0; i < kUnit / 4; i++) {
-                            const int q = 4 * i - (int)pad;  // frame offset of this word
-                            uint32_t w = 0;
-                            if (q >= 0) {
-                                w = ld32(fp + q);
-                                if (q < 4) w ^= seed >> (8 * q);
-                            } else if (q > -4) {
-                                w = (ld32(fp) ^ seed) << (8 * (-q));
-                            }
-                            acc = s4_step(acc, w, sb);
-                        }
-                    }
+        const uint32_t U = L ? (L + UNIT - 1) / UNIT : 1u;
+        const uint32_t R = active ? (U + V - 1) / V : 0u;
+        const uint32_t pad = U * UNIT - L;
+        // Steady-state cursor: this lane's chain-0 unit of round 1.
+        const uint8_t *up = fp + ((uint64_t)((int)U - V * (int)R + g) + V) * UNIT - pad;
+        uint32_t nxt[PF ? CH : 1][PF ? W : 1];
+        if (PF && R > 1) load_round<CH, G, UNIT>(reinterpret_cast<uint32_t(&)[CH][W]>(nxt), up);
+        uint32_t acc[CH];
+#pragma unroll
+        for (int c = 0; c < CH; c++) acc[c] = 0;
+        if (R > 0) {
+            // Round 0 is the only one that can hold a virtual lane's unit 0
+            // (front padding, seed, tiny frames) or no unit at all; registers
+            // are still zero, so no gap step. Chains run one after another
+            // here to keep register pressure low.
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                uint32_t w[W];
+                bool tiny;
+                load_unit<UNIT>(w, (int)U - V * (int)R + g + G * c, fp, L, pad, seed, tiny);
+                uint32_t a = 0;
+#pragma unroll
+                for (int i = 0; i < W; i++) a = s4_step(a, w[i], sb);
+                if (tiny) {  // L < 4: crc state of the few bytes straight from the seed
+                    a = seed;
+                    for (uint32_t i = 0; i < L; i++) a = byte_step(a, fp[i], sb);
                 }
+                acc[c] = a;
             }
         }
-        // Merge the G lane registers: left half advanced by UNIT * 2^j bytes.
+        // Steady state: every virtual lane has a full unit u >= 1 in rounds 1..R-1.
+        for (uint32_t k = 1; k < R; k++, up += (uint64_t)V * UNIT) {
+            uint32_t w[CH][W];
+            if (PF) {
+#pragma unroll
+                for (int c = 0; c < CH; c++)
+#pragma unroll
+                    for (int i = 0; i < W; i++) w[c][i] = nxt[PF ? c : 0][PF ? i : 0];
+                if (k + 1 < R) load_round<CH, G, UNIT>(reinterpret_cast<uint32_t(&)[CH][W]>(nxt), up + (uint64_t)V * UNIT);
+            } else {
+                load_round<CH, G, UNIT>(w, up);
+            }
+            // Seed bytes that did not fit in a unit 0 holding < 4 real bytes
+            // land in the first word of unit 1 (k == 1, virtual lane 0).
+            if (k == 1 && g == 0 && pad > UNIT - 4 && (int)U - V * (int)(R - 1) == 1)
+                w[0][0] ^= seed >> (8 * (UNIT - pad));
+            if (V > 1) {
+#pragma unroll
+                for (int c = 0; c < CH; c++) acc[c] = gap_step(acc[c], lo4);
+            }
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+#pragma unroll
+                for (int c = 0; c < CH; c++) acc[c] = s4_step(acc[c], w[c][i], sb);
+            }
+        }
+        // Merge virtual lanes: level j joins blocks of 2^j virtual lanes, the
+        // left one advanced by UNIT * 2^j bytes. Levels below log2(G) cross
+        // lanes (__shfl_xor); the rest combine the chains inside a lane.
 #pragma unroll
         for (int j = 0; (1 << j) < G; j++) {
-            const uint32_t other = __shfl_xor(acc, 1 << j);
             const bool right = (g >> j) & 1;
-            const uint32_t left = right ? other : acc;
-            const uint32_t rgt = right ? acc : other;
-            acc = bitmatrix_apply(left, p.tree[j]) ^ rgt;
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const uint32_t other = __shfl_xor(acc[c], 1 << j);
+                const uint32_t left = right ? other : acc[c];
+                const uint32_t rgt = right ? acc[c] : other;
+                acc[c] = bitmatrix_apply(left, p.tree[j]) ^ rgt;
+            }
         }
+        constexpr int kLaneLevels = (G >= 64) ? 6 : (G >= 32) ? 5 : (G >= 16) ? 4 : (G >= 8) ? 3 : (G >= 4) ? 2 : (G >= 2) ? 1 : 0;
+#pragma unroll
+        for (int span = 1, lvl = kLaneLevels; span < CH; span <<= 1, lvl++) {
+#pragma unroll
+            for (int c = 0; c + span < CH; c += 2 * span) acc[c] = bitmatrix_apply(acc[c], p.tree[lvl]) ^ acc[c + span];
+        }
+        const uint32_t total = acc[0];
         if (active && g == G - 1) {
-            const uint32_t crc = acc ^ p.xorout;
+            const uint32_t crc = total ^ p.xorout;
             if (p.out_crc) p.out_crc[f] = crc;
             if (p.verify) {
                 const bool good = (crc == ld32(fp + L));
@@ -366,49 +451,115 @@ val_status_t bind_thread()
 }
 
 bool valid_lanes(uint32_t g) { return g == 1 || g == 2 || g == 4 || g == 8 || g == 16 || g == 32 || g == 64; }
+bool valid_chains(uint32_t c) { return c == 1 || c == 2; }
 
 std::atomic<uint32_t> g_forced_lanes{0};
+std::atomic<uint32_t> g_forced_chains{0};
 
+uint32_t env_u32(const char *name)
+{
+    const char *e = getenv(name);
+    return e ? (uint32_t)atoi(e) : 0u;
+}
+
+// Lanes that share one frame (G). Short frames share a wave (64/G frames per
+// wave); long frames spread over more lanes so every lane hashes a few KiB.
 uint32_t lanes_per_frame(uint32_t len)
 {
-    static const uint32_t env_g = [] {
-        const char *e = getenv("VAL_GPU_LANES_PER_FRAME");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
+    static const uint32_t env_g = env_u32("VAL_GPU_LANES_PER_FRAME");
     const uint32_t forced = g_forced_lanes.load(std::memory_order_relaxed);
     if (valid_lanes(forced)) return forced;
     if (valid_lanes(env_g)) return env_g;
-    // ~2 KiB of CRC input per lane keeps the merge tree cheap; shorter frames
-    // share a wave (64/G frames per wave).
-    uint32_t g = 1;
-    while (g < 64 && (uint64_t)len >= (uint64_t)g * 2u * 2048u) g <<= 1;
+    // Measured on MI355X (tools/sweep_geometry.py): ~2 KiB of CRC input per
+    // lane, at least 4 and at most 32 lanes per frame.
+    uint32_t g = 4;
+    while (g < 32 && (uint64_t)len >= (uint64_t)g * 2u * 2048u) g <<= 1;
     return g;
 }
 
-void fill_geometry(FrameParams &p, uint32_t G)
+// Independent CRC chains per lane (CH): more loads and LDS lookups in flight.
+uint32_t chains_per_lane(uint32_t len)
 {
-    for (int k = 0; k < 4; k++) p.xtab[k] = gf2_x8n((uint64_t)(k + 1));
-    p.xgap = gf2_x8n((uint64_t)(G - 1) * kUnit);
-    for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)kUnit << j, p.tree[j]);
+    static const uint32_t env_c = env_u32("VAL_GPU_CHAINS_PER_LANE");
+    const uint32_t forced = g_forced_chains.load(std::memory_order_relaxed);
+    if (valid_chains(forced)) return forced;
+    if (valid_chains(env_c)) return env_c;
+    (void)len;
+    return 1;
 }
 
-val_status_t launch_frames(FrameParams &p, uint32_t G, hipStream_t s)
+bool valid_unit(uint32_t u) { return u == 64 || u == 128; }
+std::atomic<uint32_t> g_forced_unit{0};
+std::atomic<int> g_forced_prefetch{-1};
+
+// Bytes a lane hashes per round.
+uint32_t unit_bytes(uint32_t len)
+{
+    static const uint32_t env_u = env_u32("VAL_GPU_UNIT");
+    const uint32_t forced = g_forced_unit.load(std::memory_order_relaxed);
+    if (valid_unit(forced)) return forced;
+    if (valid_unit(env_u)) return env_u;
+    (void)len;
+    return 64;
+}
+
+bool prefetch_on(uint32_t len)
+{
+    static const int env_p = getenv("VAL_GPU_PREFETCH") ? atoi(getenv("VAL_GPU_PREFETCH")) : -1;
+    const int forced = g_forced_prefetch.load(std::memory_order_relaxed);
+    if (forced >= 0) return forced != 0;
+    if (env_p >= 0) return env_p != 0;
+    (void)len;
+    return true;
+}
+
+void fill_geometry(FrameParams &p, uint32_t V, uint32_t unit)
+{
+    for (int k = 0; k < 4; k++) p.xtab[k] = gf2_x8n((uint64_t)(k + 1));
+    p.xgap = gf2_x8n((uint64_t)(V - 1) * unit);
+    for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)unit << j, p.tree[j]);
+}
+
+template <int G, int UNIT, bool PF>
+void launch_gup(uint32_t CH, dim3 grid, dim3 block, hipStream_t s, const FrameParams &p)
+{
+    if (CH == 2) hipLaunchKernelGGL((k_frames<G, 2, UNIT, PF>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((k_frames<G, 1, UNIT, PF>), grid, block, 0, s, p);
+}
+
+template <int G>
+void launch_g(uint32_t CH, uint32_t unit, bool pf, dim3 grid, dim3 block, hipStream_t s, const FrameParams &p)
+{
+    if (unit == 128) {
+        if (pf) launch_gup<G, 128, true>(CH, grid, block, s, p);
+        else launch_gup<G, 128, false>(CH, grid, block, s, p);
+    } else {
+        if (pf) launch_gup<G, 64, true>(CH, grid, block, s, p);
+        else launch_gup<G, 64, false>(CH, grid, block, s, p);
+    }
+}
+
+val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
 {
     if (p.n == 0) return VAL_OK;
-    fill_geometry(p, G);
+    const uint32_t G = lanes_per_frame(typical_len);
+    const uint32_t CH = chains_per_lane(typical_len);
+    const uint32_t unit = unit_bytes(typical_len);
+    const bool pf = prefetch_on(typical_len);
+    fill_geometry(p, G * CH, unit);
     const uint64_t groups_per_block = (uint64_t)(kBlock / 64) * (64 / G);
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
     blocks = std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus);  // one 144 KiB-LDS workgroup per CU, persistent
     if (blocks == 0) blocks = 1;
     dim3 grid((unsigned)blocks), block(kBlock);
     switch (G) {
-    case 1: hipLaunchKernelGGL(k_frames<1>, grid, block, 0, s, p); break;
-    case 2: hipLaunchKernelGGL(k_frames<2>, grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL(k_frames<4>, grid, block, 0, s, p); break;
-    case 8: hipLaunchKernelGGL(k_frames<8>, grid, block, 0, s, p); break;
-    case 16: hipLaunchKernelGGL(k_frames<16>, grid, block, 0, s, p); break;
-    case 32: hipLaunchKernelGGL(k_frames<32>, grid, block, 0, s, p); break;
-    case 64: hipLaunchKernelGGL(k_frames<64>, grid, block, 0, s, p); break;
+    case 1: launch_g<1>(CH, unit, pf, grid, block, s, p); break;
+    case 2: launch_g<2>(CH, unit, pf, grid, block, s, p); break;
+    case 4: launch_g<4>(CH, unit, pf, grid, block, s, p); break;
+    case 8: launch_g<8>(CH, unit, pf, grid, block, s, p); break;
+    case 16: launch_g<16>(CH, unit, pf, grid, block, s, p); break;
+    case 32: launch_g<32>(CH, unit, pf, grid, block, s, p); break;
+    case 64: launch_g<64>(CH, unit, pf, grid, block, s, p); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
@@ -444,7 +595,7 @@ val_status_t region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, u
         p.seed0 = p.seed_rest = state_in;
         p.xorout = 0;
         p.out_crc = d_out;
-        return launch_frames(p, lanes_per_frame((uint32_t)len), s);
+        return launch_frames(p, (uint32_t)len, s);
     }
     uint32_t *d_states = nullptr;
     VCRC_HIP(hipMallocAsync((void **)&d_states, (size_t)n * 4u, s), "hipMallocAsync(region scratch)");
@@ -458,7 +609,7 @@ val_status_t region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, u
     p.seed_rest = 0;
     p.xorout = 0;
     p.out_crc = d_states;
-    val_status_t st = launch_frames(p, lanes_per_frame((uint32_t)clen), s);
+    val_status_t st = launch_frames(p, (uint32_t)clen, s);
     if (st != VAL_OK) {
         (void)hipFreeAsync(d_states, s);
         return st;
@@ -575,7 +726,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     p.out_ok = ok ? d_ok : nullptr;
     p.nbad = d_nbad;
     const uint32_t typical = n ? (uint32_t)std::min<uint64_t>(len_sum / n, 0xFFFFFFFFu) : 0u;
-    if ((st = launch_frames(p, lanes_per_frame(typical), s)) != VAL_OK) return st;
+    if ((st = launch_frames(p, typical, s)) != VAL_OK) return st;
     if (crc) VCRC_HIP(hipMemcpyAsync(crc, d_crc, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H crc");
     if (hdr) VCRC_HIP(hipMemcpyAsync(hdr, d_hdr, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H hdr");
     if (ok) VCRC_HIP(hipMemcpyAsync(ok, d_ok, (size_t)n, hipMemcpyDeviceToHost, s), "D2H ok");
@@ -634,6 +785,28 @@ val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes)
     return VAL_OK;
 }
 
+uint32_t val_gpu_chains_per_lane(uint32_t typical_len) { return chains_per_lane(typical_len); }
+
+val_status_t val_gpu_set_unit_bytes(uint32_t unit)
+{
+    if (unit != 0 && !valid_unit(unit)) return fail(VAL_ERR_INVALID_ARG, "unit must be 0, 64 or 128");
+    g_forced_unit.store(unit, std::memory_order_relaxed);
+    return VAL_OK;
+}
+
+val_status_t val_gpu_set_prefetch(int on)
+{
+    g_forced_prefetch.store(on < 0 ? -1 : (on ? 1 : 0), std::memory_order_relaxed);
+    return VAL_OK;
+}
+
+val_status_t val_gpu_set_chains_per_lane(uint32_t chains)
+{
+    if (chains != 0 && !valid_chains(chains)) return fail(VAL_ERR_INVALID_ARG, "chains must be 0, 1 or 2");
+    g_forced_chains.store(chains, std::memory_order_relaxed);
+    return VAL_OK;
+}
+
 uint32_t val_crc32_shift(uint32_t state, uint64_t nbytes) { return gf2_mul(gf2_x8n(nbytes), state); }
 
 uint32_t val_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
@@ -682,7 +855,7 @@ val_status_t val_crc32_frames_dev(const uint8_t *d_base, const uint64_t *d_off, 
     p.out_crc = d_crc;
     p.out_hdr = d_hdr;
     const uint32_t typical = d_off ? (len_hint ? len_hint : 16384u) : flen;
-    return launch_frames(p, lanes_per_frame(typical), pick_stream(stream));
+    return launch_frames(p, typical, pick_stream(stream));
 }
 
 val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
@@ -710,7 +883,7 @@ val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *
     p.out_ok = d_ok;
     p.nbad = d_nbad;
     const uint32_t typical = d_off ? (len_hint ? len_hint : 16384u) : flen;
-    return launch_frames(p, lanes_per_frame(typical), pick_stream(stream));
+    return launch_frames(p, typical, pick_stream(stream));
 }
 
 val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_state_out,
