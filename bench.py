@@ -28,11 +28,13 @@ GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 CONFIGS = {
-    # name: (frames per GPU, payload bytes, explicit offset, header_crc)
+    # name: (frames per GPU, payload bytes, explicit offset, header_crc); cfg5 is ragged (make_ragged_frames)
     "cfg3": (1 << 20, 16384, True, True),
     "cfg2": (1 << 16, 1024, True, False),
     "cfg4": (131113, 65516, True, False),
+    "cfg5": (262144, 0, True, True),
 }
+CFG5_MIN, CFG5_MAX = 512, 65516  # payload bytes, log-uniform (BASELINE configs[4])
 
 
 def parse():
@@ -45,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--host-inclusive", action="store_true", help="also time H2D+kernel+D2H (stderr)")
+    ap.add_argument("--sort-frames", action="store_true", help="cfg5: order descriptors by length (diagnostic)")
     return ap.parse_args()
 
 
@@ -67,6 +70,36 @@ def make_frames(torch, dev, n, payload, explicit, first_index, seed):
         buf[:, 8:16] = offs.view(torch.uint8).view(n, 8)
     buf[:, flen:] = 0
     return buf, flen, stride
+
+
+def make_ragged_frames(torch, dev, n, seed):
+    """cfg5: n DATA frames, payload log-uniform in [512, 65516], one in 8 with
+    an implied offset (content = payload, src/val_sender.c:833), packed back to
+    back so frame starts are byte-unaligned. Returns (stream, off, len) with
+    off/len as GPU tensors (int64 / int32) and len = CRC input bytes."""
+    rng = np.random.default_rng(seed)
+    pay = np.exp(rng.uniform(np.log(CFG5_MIN), np.log(CFG5_MAX), n)).astype(np.int64)
+    explicit = (np.arange(n) % 8) != 7
+    content = pay + 8 * explicit
+    crc_len = 8 + content
+    wire = crc_len + 4
+    off = np.concatenate([[0], np.cumsum(wire)[:-1]]).astype(np.int64)
+    total = int(wire.sum())
+    g = torch.Generator(device=dev).manual_seed(seed)
+    buf = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    hdr = np.zeros((n, 8), np.uint8)
+    hdr[:, 0] = 5
+    hdr[:, 1] = explicit.astype(np.uint8)
+    hdr[:, 2] = content & 0xFF
+    hdr[:, 3] = content >> 8
+    d_off = torch.from_numpy(off).to(dev)
+    idx = (d_off[:, None] + torch.arange(8, device=dev)[None, :]).reshape(-1)
+    buf[idx] = torch.from_numpy(hdr.reshape(-1)).to(dev)
+    file_off = np.concatenate([[0], np.cumsum(pay)[:-1]]).astype(np.int64)
+    ex = np.nonzero(explicit)[0]
+    idx = (d_off[ex][:, None] + 8 + torch.arange(8, device=dev)[None, :]).reshape(-1)
+    buf[idx] = torch.from_numpy(file_off[ex].astype("<i8").view(np.uint8)).to(dev)
+    return buf, d_off, torch.from_numpy(crc_len.astype(np.int32)).to(dev)
 
 
 def cpu_baseline(sample: np.ndarray, stride: int, flen: int, n: int, threads: int):
@@ -122,32 +155,55 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)  # == local on a full node; lets a 1-GPU box rehearse N ranks
+    backend = os.environ.get("VAL_BENCH_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{gpu}")
     torch.cuda.set_device(dev)
 
     import val_protocol_amd.crc as vc
 
-    vc.init(local)
+    vc.init(gpu)
     n, payload, explicit, header = CONFIGS[args.config]
-    buf, flen, stride = make_frames(torch, dev, n, payload, explicit, rank * n, seed=1234 + rank)
-    flat = buf.view(-1)
+    ragged = args.config == "cfg5"
+    d_off = d_len = None
+    if ragged:
+        buf, d_off, d_len = make_ragged_frames(torch, dev, n, seed=1234 + rank)
+        if args.sort_frames:
+            perm = torch.argsort(d_len)
+            d_off, d_len = d_off[perm].contiguous(), d_len[perm].contiguous()
+        flen, stride = 0, 0
+        flat = buf
+        len_hint = 0  # mixed lengths: the library bins frames by length class on the device
+    else:
+        buf, flen, stride = make_frames(torch, dev, n, payload, explicit, rank * n, seed=1234 + rank)
+        flat = buf.view(-1)
+        len_hint = flen
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
     nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    kw = dict(off=d_off, length=d_len, n=n, len_hint=len_hint) if ragged else dict(stride=stride, flen=flen, n=n)
     if args.verify:  # trailers must be valid first
-        vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc)
-        buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
+        vc.frames(flat, out_crc=crc, **kw)
+        if ragged:
+            tidx = ((d_off + d_len.long())[:, None] + torch.arange(4, device=dev)[None, :]).reshape(-1)
+            flat[tidx] = crc.view(torch.uint8)
+        else:
+            buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
 
     def step():
         if args.verify:
-            vc.verify_frames(flat, stride=stride, flen=flen, n=n, out_ok=ok, nbad=nbad, out_hdr=hdr)
+            vc.verify_frames(flat, out_ok=ok, nbad=nbad, out_hdr=hdr, **kw)
         else:
-            vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+            vc.frames(flat, out_crc=crc, out_hdr=hdr, **kw)
 
     for _ in range(args.warmup):
         step()
@@ -168,29 +224,38 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
     # Parity spot check of this run's output against the oracle (not timed).
     sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, 256, replace=False), [0, n - 1]]))
-    rows = buf[torch.from_numpy(sample_idx).to(dev)].cpu().numpy().reshape(-1)
     from tests import _oracle
 
-    want = _oracle.frames_strided(rows, stride, flen, sample_idx.size)
+    if ragged:
+        o = d_off.cpu().numpy()[sample_idx]
+        l = d_len.cpu().numpy()[sample_idx].astype(np.int64)
+        pieces = [flat[int(a):int(a) + int(b)].cpu().numpy() for a, b in zip(o, l)]
+        rows = np.concatenate(pieces)
+        so = np.concatenate([[0], np.cumsum(l)[:-1]]).astype(np.uint64)
+        want = _oracle.frames(rows, so, l.astype(np.uint32))
+    else:
+        rows = buf[torch.from_numpy(sample_idx).to(dev)].cpu().numpy().reshape(-1)
+        want = _oracle.frames_strided(rows, stride, flen, sample_idx.size)
     got = crc.cpu().numpy().view(np.uint32)[sample_idx] if not args.verify else want
     parity = bool(np.array_equal(got, want))
     if args.verify:
         parity = parity and int(nbad.item()) == 0
 
-    bytes_per_launch = n * flen  # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
+    # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
+    bytes_per_launch = int(d_len.long().sum().item()) if ragged else n * flen
     total_bytes = bytes_per_launch * args.steps * world
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
 
-    if args.host_inclusive and rank == 0:
+    if args.host_inclusive and rank == 0 and not ragged:
         host = buf.cpu().numpy().reshape(-1)
         t1 = time.perf_counter()
         for _ in range(2):
@@ -199,7 +264,7 @@ def main():
         print(f"[bench] host-inclusive (pageable H2D + kernel + D2H): {hi:.2f} GiB/s", file=sys.stderr)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not ragged:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         ns = min(n, max(1, (1 << 30) // flen))  # ~1 GiB host sample of the same frames
         host_rows = buf[:ns].cpu().numpy().reshape(-1)
@@ -226,13 +291,15 @@ def main():
             "dtype": "u32",
             "data": "synthetic (device-generated random payloads, reference DATA framing)",
             "config": {
-                "workload": f"{args.config}: {n} DATA frames x {payload} B payload per GPU, "
-                            f"{'header_crc + ' if header else ''}trailer CRC-32"
-                            f"{' (RX verify)' if args.verify else ''}",
+                "workload": (f"{args.config}: {n} DATA frames x "
+                             + (f"{CFG5_MIN}-{CFG5_MAX} B log-uniform payload (1 in 8 implied offset), packed unaligned"
+                                if ragged else f"{payload} B payload") + " per GPU, "
+                             f"{'header_crc + ' if header else ''}trailer CRC-32"
+                             f"{' (RX verify)' if args.verify else ''}"),
                 "frames_per_gpu": n,
-                "crc_input_bytes_per_frame": flen,
-                "frame_stride": stride,
-                "lanes_per_frame": vc.lanes_per_frame(flen),
+                "crc_input_bytes_per_frame": (bytes_per_launch / n) if ragged else flen,
+                "frame_stride": stride if not ragged else "packed",
+                "lanes_per_frame": "per length class (2/4/8/16)" if ragged else vc.lanes_per_frame(len_hint),
                 "parallelism": f"frame-sharded x{world} (no collective)",
                 "parity_sample_ok": parity,
             },

@@ -65,8 +65,11 @@ uint32_t val_crc32_shift(uint32_t state, uint64_t nbytes);
  * Outputs (device, n entries, any may be NULL):
  *   d_crc[i] = CRC-32 of frame i (the trailer value)
  *   d_hdr[i] = header_crc = CRC-32 of the first min(8, len_i) bytes
- * len_hint: typical frame length, picks the lanes-per-frame geometry in
- * descriptor mode (0 = 16 KiB). Lengths may be 0 .. 2^32-1.            */
+ * len_hint (descriptor mode): typical frame length when the batch is
+ * uniform (picks the lanes-per-frame geometry directly); 0 = lengths mixed or
+ * unknown: frames are binned by length class on the device and each class
+ * runs its own geometry (ragged path, no host synchronisation).
+ * Lengths may be 0 .. 2^32-1.                                          */
 val_status_t val_crc32_frames_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t stride,
                                   uint32_t flen, uint32_t n, uint32_t len_hint, uint32_t *d_crc, uint32_t *d_hdr,
                                   void *stream);
@@ -105,11 +108,6 @@ uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);
  * process; 0 restores the automatic choice. Returns VAL_ERR_INVALID_ARG for
  * other values. Results never depend on it; only speed does. */
 val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
-/* Independent CRC chains each lane runs (1 or 2; 0 = automatic). */
-uint32_t val_gpu_chains_per_lane(uint32_t typical_len);
-val_status_t val_gpu_set_chains_per_lane(uint32_t chains);
-/* Bytes a lane hashes per round (64 or 128; 0 = automatic). */
-val_status_t val_gpu_set_unit_bytes(uint32_t unit);
 /* Register prefetch of the next round (1 on, 0 off, -1 automatic). */
 val_status_t val_gpu_set_prefetch(int on);
 

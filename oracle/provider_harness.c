@@ -16,6 +16,14 @@
  *       frames fed to val_internal_recv_packet (src/val_core.c:880) with the
  *       GPU provider: clean frames -> VAL_OK, corrupted -> VAL_ERR_CRC and
  *       metrics.crc_errors++.
+ *   provider_harness <libval_crc_hip.so> window <W> <mtu>
+ *       a window of W DATA frames framed by the reference
+ *       TX path one by one (built-in CRC) vs the batched path of this build
+ *       (val_frame_data_batch + one val_crc32_frames_host launch +
+ *       val_frame_put_trailers): byte-identical streams required. Then the
+ *       stream, with some frames corrupted, goes through the reference RX
+ *       (val_internal_recv_packet per frame) and through val_frame_scan +
+ *       one val_crc32_verify_frames_host launch: same verdict per frame.
  *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
  *       full val_send_files / val_receive_files transfer over an in-memory
  *       duplex pipe (the reference test strategy), provider on
@@ -255,6 +263,105 @@ static int mode_rx(void)
     return 0;
 }
 
+
+typedef int (*fn_batch_t)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, const uint8_t *, uint32_t,
+                          uint8_t *, size_t, uint64_t *, uint32_t *, size_t *);
+typedef int (*fn_frames_host_t)(const uint8_t *, uint64_t, const uint64_t *, const uint32_t *, uint64_t, uint32_t, uint32_t,
+                                uint32_t *, uint32_t *);
+typedef void (*fn_put_t)(uint8_t *, const uint64_t *, const uint32_t *, const uint32_t *, uint32_t);
+typedef int (*fn_scan_t)(const uint8_t *, size_t, size_t, uint32_t, uint64_t *, uint32_t *, uint32_t *, size_t *);
+typedef int (*fn_verify_t)(const uint8_t *, uint64_t, const uint64_t *, const uint32_t *, uint64_t, uint32_t, uint32_t,
+                           uint8_t *, uint32_t *);
+static void *g_lib;
+
+static int mode_window(uint32_t W, size_t mtu)
+{
+    fn_batch_t batch = (fn_batch_t)dlsym(g_lib, "val_frame_data_batch");
+    fn_frames_host_t frames = (fn_frames_host_t)dlsym(g_lib, "val_crc32_frames_host");
+    fn_put_t put = (fn_put_t)dlsym(g_lib, "val_frame_put_trailers");
+    fn_scan_t scan = (fn_scan_t)dlsym(g_lib, "val_frame_scan");
+    fn_verify_t verify = (fn_verify_t)dlsym(g_lib, "val_crc32_verify_frames_host");
+    if (!batch || !frames || !put || !scan || !verify) return 2;
+    /* The sender's window: max payload MTU-12, minus 8 with an explicit offset
+       (src/val_sender.c:271-277); offset explicit on the first frame of the
+       window (include_offset = next_to_send == last_acked, :833). */
+    const size_t maxp = mtu - 12;
+    const uint64_t file_size = (uint64_t)W * maxp - 777u;
+    uint8_t *file = (uint8_t *)malloc(file_size);
+    oracle_prng_fill(0x3171D0, file, file_size);
+    uint64_t *pay_off = calloc(W, 8), *file_off = calloc(W, 8), *fo = calloc(W, 8), *fo2 = calloc(W, 8);
+    uint32_t *pay_len = calloc(W, 4), *cl = calloc(W, 4), *cl2 = calloc(W, 4), *crc = calloc(W, 4);
+    uint8_t *inc = calloc(W, 1), *ok = calloc(W, 1);
+    uint32_t nf = 0;
+    for (uint64_t pos = 0; pos < file_size && nf < W; nf++) {
+        inc[nf] = (nf % 5 == 0);
+        size_t take = maxp - (inc[nf] ? 8u : 0u);
+        if (take > file_size - pos) take = (size_t)(file_size - pos);
+        pay_off[nf] = pos;
+        file_off[nf] = pos;
+        pay_len[nf] = (uint32_t)take;
+        pos += take;
+    }
+    /* reference TX, one frame at a time */
+    pipe_t a;
+    pipe_init(&a, (size_t)W * mtu + 4096);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, NULL);
+    val_session_t *s = NULL;
+    if (val_session_create(&cfg, &s, NULL) != VAL_OK) return 3;
+    for (uint32_t i = 0; i < nf; i++)
+        if (val_internal_send_packet_ex(s, VAL_PKT_DATA, file + pay_off[i], pay_len[i], file_off[i], inc[i]) != VAL_OK) return 4;
+    const size_t ref_len = a.len;
+    uint8_t *ref = (uint8_t *)malloc(ref_len);
+    pipe_pop(&a, ref, ref_len, 10);
+    /* batched TX on the GPU */
+    uint8_t *stage = (uint8_t *)malloc((size_t)W * mtu);
+    size_t used = 0;
+    int st = batch(file, pay_off, pay_len, file_off, inc, nf, stage, (size_t)W * mtu, fo, cl, &used);
+    if (st != 0) return 5;
+    st = frames(stage, used, fo, cl, 0, 0, nf, crc, NULL);
+    if (st != 0) return 6;
+    put(stage, fo, cl, crc, nf);
+    const int tx_equal = (used == ref_len) && memcmp(stage, ref, ref_len) == 0;
+    /* corrupt some frames of the reference stream, then verify both ways */
+    uint32_t corrupted = 0;
+    for (uint32_t i = 3; i < nf; i += 7) {
+        ref[fo[i] + 8u + (i * 13u) % (cl[i] - 8u)] ^= (uint8_t)(1u << (i % 8));
+        corrupted++;
+    }
+    uint32_t nscan = 0;
+    size_t consumed = 0;
+    st = scan(ref, ref_len, mtu, nf, fo2, cl2, &nscan, &consumed);
+    uint32_t nbad = 0;
+    int vst = verify(ref, ref_len, fo2, cl2, 0, 0, nscan, ok, &nbad);
+    pipe_push(&a, ref, ref_len);
+    val_config_t rcfg;
+    make_cfg(&rcfg, &e, mtu, NULL);
+    val_session_t *r = NULL;
+    if (val_session_create(&rcfg, &r, NULL) != VAL_OK) return 7;
+    uint8_t *out = (uint8_t *)malloc(mtu);
+    uint32_t same_verdict = 0, ref_bad = 0;
+    for (uint32_t i = 0; i < nf; i++) {
+        val_packet_type_t t = 0;
+        uint32_t plen = 0;
+        uint64_t off = 0;
+        int rc = val_internal_recv_packet(r, &t, out, (uint32_t)mtu, &plen, &off, 100);
+        ref_bad += (rc == VAL_ERR_CRC);
+        same_verdict += ((rc == VAL_OK) == (i < nscan && ok[i] == 1));
+    }
+    val_metrics_t m;
+    memset(&m, 0, sizeof m);
+    val_get_metrics(r, &m);
+    printf("{\"mode\":\"window\",\"frames\":%u,\"mtu\":%zu,\"wire_bytes\":%zu,\"tx_equal\":%d,\"scan_status\":%d,\"scanned\":%u,"
+           "\"consumed\":%zu,\"verify_status\":%d,\"gpu_bad\":%u,\"ref_bad\":%u,\"ref_crc_errors\":%u,\"corrupted\":%u,"
+           "\"same_verdict\":%u}\n",
+           nf, mtu, ref_len, tx_equal, st, nscan, consumed, vst, nbad, ref_bad, m.crc_errors, corrupted, same_verdict);
+    val_session_destroy(s);
+    val_session_destroy(r);
+    return 0;
+}
+
 typedef struct {
     val_session_t *rx;
     const char *dir;
@@ -339,6 +446,7 @@ int main(int argc, char **argv)
     int use_gpu = strcmp(argv[1], "none") != 0;
     if (use_gpu) {
         void *h = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
+        g_lib = h;
         if (!h) {
             fprintf(stderr, "dlopen: %s\n", dlerror());
             return 1;
@@ -354,6 +462,8 @@ int main(int argc, char **argv)
     }
     if (!strcmp(argv[2], "tx")) return use_gpu ? mode_tx() : 1;
     if (!strcmp(argv[2], "rx")) return use_gpu ? mode_rx() : 1;
+    if (!strcmp(argv[2], "window") && argc >= 5)
+        return use_gpu ? mode_window((uint32_t)strtoul(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0)) : 1;
     if (!strcmp(argv[2], "loopback") && argc >= 5)
         return mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu);
     fprintf(stderr, "bad mode\n");

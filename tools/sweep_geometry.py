@@ -2,7 +2,7 @@
 """Times the frames kernel for kernel geometries on the BASELINE shapes
 (device-resident, HIP events on the launch stream). Diagnostic only.
 
-SWEEP_COMBOS="G:CH:UNIT:PF,..." overrides the default list."""
+SWEEP_COMBOS="G:PF,..." overrides the default list."""
 import os
 import sys
 
@@ -14,9 +14,9 @@ import bench  # noqa: E402
 import val_protocol_amd.crc as vc  # noqa: E402
 
 DEFAULT = {
-    "cfg3": [(g, c, u, p) for g in (4, 8, 16, 32) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (1, 128, 1), (2, 64, 0))],
-    "cfg4": [(g, c, u, p) for g in (8, 16, 32, 64) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (1, 128, 1), (2, 64, 0))],
-    "cfg2": [(g, c, u, p) for g in (1, 2, 4, 8) for (c, u, p) in ((1, 64, 0), (1, 64, 1), (1, 128, 0), (2, 64, 0))],
+    "cfg3": [(g, p) for g in (4, 8, 16, 32) for p in (0, 1)],
+    "cfg4": [(g, p) for g in (8, 16, 32, 64) for p in (0, 1)],
+    "cfg2": [(g, p) for g in (1, 2, 4, 8) for p in (0, 1)],
 }
 
 
@@ -50,12 +50,12 @@ def main():
         vc.set_geometry()
         vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
         ref = crc.clone()
-        for G, CH, U, PF in combos:
-            vc.set_geometry(G, CH, U, PF)
+        for G, PF in combos:
+            vc.set_geometry(G, PF)
             med, best = time_it(lambda: vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr))
             same = bool(torch.equal(crc, ref))
             gbs = n * flen / (med * 1e-3) / 1e9
-            print(f"{name} G={G:2d} CH={CH} UNIT={U:3d} PF={PF}: median {med:.3f} ms best {best:.3f} ms "
+            print(f"{name} G={G:2d} PF={PF}: median {med:.3f} ms best {best:.3f} ms "
                   f"{gbs:7.1f} GB/s same={same}", flush=True)
         vc.set_geometry()
         del buf, flat

@@ -36,7 +36,7 @@ LIB_PATH = os.path.join(_HERE, "libval_crc_hip.so")
 EXPORTS = (
     "val_gpu_init", "val_gpu_shutdown", "val_gpu_device_count", "val_gpu_abi_version",
     "val_gpu_last_error", "val_gpu_lanes_per_frame", "val_gpu_set_lanes_per_frame",
-    "val_gpu_chains_per_lane", "val_gpu_set_chains_per_lane", "val_gpu_set_unit_bytes", "val_gpu_set_prefetch",
+    "val_gpu_set_prefetch",
     "val_gpu_crc32_provider", "val_crc32_combine", "val_crc32_shift",
     "val_crc32", "val_crc32_init_state", "val_crc32_update_state", "val_crc32_finalize_state",
     "val_crc32_frames_dev", "val_crc32_verify_frames_dev", "val_crc32_region_dev",
@@ -74,9 +74,6 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_gpu_last_error", ctypes.c_char_p)
     fn("val_gpu_lanes_per_frame", u32, u32)
     fn("val_gpu_set_lanes_per_frame", i32, u32)
-    fn("val_gpu_chains_per_lane", u32, u32)
-    fn("val_gpu_set_chains_per_lane", i32, u32)
-    fn("val_gpu_set_unit_bytes", i32, u32)
     fn("val_gpu_set_prefetch", i32, ctypes.c_int)
     fn("val_gpu_crc32_provider", u32, u32, _vp, sz)
     fn("val_crc32_combine", u32, u32, u32, u64)
@@ -181,29 +178,14 @@ def lanes_per_frame(typical_len: int) -> int:
     return int(lib().val_gpu_lanes_per_frame(typical_len))
 
 
-def chains_per_lane(typical_len: int) -> int:
-    return int(lib().val_gpu_chains_per_lane(typical_len))
-
-
-def set_chains_per_lane(chains: int) -> None:
-    """Force the independent chains per lane (0 = automatic). Speed only."""
-    _check(lib().val_gpu_set_chains_per_lane(chains), "val_gpu_set_chains_per_lane")
-
-
-def set_unit_bytes(unit: int) -> None:
-    """Force bytes per lane per round (64/128, 0 = automatic). Speed only."""
-    _check(lib().val_gpu_set_unit_bytes(unit), "val_gpu_set_unit_bytes")
-
-
 def set_prefetch(on: int) -> None:
     """Register prefetch of the next round: 1 on, 0 off, -1 automatic."""
     _check(lib().val_gpu_set_prefetch(on), "val_gpu_set_prefetch")
 
 
-def set_geometry(lanes: int = 0, chains: int = 0, unit: int = 0, prefetch: int = -1) -> None:
+def set_geometry(lanes: int = 0, prefetch: int = -1) -> None:
+    """Force lanes per frame (0 = automatic) and prefetch (-1 = automatic)."""
     set_lanes_per_frame(lanes)
-    set_chains_per_lane(chains)
-    set_unit_bytes(unit)
     set_prefetch(prefetch)
 
 

@@ -1,27 +1,7 @@
-// val_crc32_hip.hip -- CDNA4 (gfx950) kernels and the C ABI of the VAL CRC-32
-// integrity path. See DESIGN.md for the roofline argument; reference call
-// sites are cited per entry point in include/val_crc32_gpu.h.
-//
-// Algorithm (no carry-less multiply on gfx950, no MFMA: this is GF(2) table
-// work, not a dense contraction):
-//   * A frame's CRC input of L bytes is cut into UNIT-byte units counted from
-//     the END of the frame; the first unit is front-padded with zeros (free:
-//     a zero register stays zero over zero bytes). The initial register
-//     ("seed", 0xFFFFFFFF for VAL) is XORed into the first four real bytes,
-//     which equals starting the register at the seed for L >= 4.
-//   * G lanes share a frame. Lane g owns units g, g+G, g+2G, ... counted so
-//     that lane G-1 owns the last unit. Each lane keeps one raw register and
-//     runs slice-by-4 over its units (4 LDS lookups per 4 bytes); between its
-//     units it advances the register over the (G-1)*UNIT bytes owned by the
-//     other lanes with 8 nibble-table lookups (the "gap" map).
-//   * A log2(G)-step __shfl_xor tree merges the G registers; step j advances
-//     the left half by UNIT*2^j bytes (32x32 GF(2) bit-matrix in SGPRs).
-//   * LDS holds the four slice tables replicated 32x across banks so the
-//     per-lane lookups of a half-wave never conflict (128 KiB), plus the gap
-//     nibble tables (16 KiB). One 1024-thread workgroup per CU.
-//   * Loads are per-lane contiguous 64-byte units (4 x dwordx4, unaligned
-//     addresses allowed): measured on MI355X this pattern streams faster than
-//     1 KiB-contiguous wave loads (bench/micro/mb1.hip).
+// val_crc32_hip.hip -- host side and C ABI of the VAL CRC-32 integrity path
+// on MI355X (gfx950). Kernels: crc_kernels.hpp; device building blocks:
+// crc_device.hpp; algorithm and roofline: DESIGN.md; reference call sites per
+// entry point: include/val_crc32_gpu.h.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -34,358 +14,11 @@
 #include <mutex>
 #include <string>
 
-#include "gf2_crc32.h"
+#include "crc_kernels.hpp"
 #include "val_crc32_gpu.h"
 #include "val_protocol.h"
 
 namespace vcrc {
-
-constexpr int kBlock = 1024;   // threads per workgroup (16 waves)
-constexpr uint32_t kLdsS4 = 0;          // 2 table pairs x 256 rows x 256 B
-constexpr uint32_t kLdsGap = 131072;    // 8 nibble tables x 16 rows x 128 B
-constexpr uint32_t kLdsWords = (131072 + 16384) / 4;
-constexpr int kMaxTree = 7;    // log2(max virtual lanes = 128)
-
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint32_t u32u __attribute__((aligned(1)));
-
-struct FrameParams {
-    const uint8_t *base;
-    const uint64_t *off;   // NULL: strided mode
-    const uint32_t *len;
-    uint64_t stride;
-    uint32_t flen;
-    uint32_t last_len;     // strided mode: length of frame n-1
-    uint32_t n;
-    uint32_t seed0;        // initial register of frame 0
-    uint32_t seed_rest;    // initial register of frames 1..n-1
-    uint32_t xorout;       // XORed into every output (0xFFFFFFFF = finalized CRC)
-    uint32_t *out_crc;
-    uint32_t *out_hdr;
-    uint8_t *out_ok;
-    uint32_t *nbad;
-    uint32_t verify;
-    uint32_t xtab[4];      // x^(8(k+1)) defining slice table T_k
-    uint32_t xgap;         // x^(8 (G-1) UNIT)
-    uint32_t tree[kMaxTree][32];  // bit-matrix columns of "advance UNIT*2^j bytes"
-};
-
-__shared__ uint32_t s_lds[kLdsWords];
-
-__device__ __forceinline__ uint32_t lds_read(uint32_t byte_addr)
-{
-    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(s_lds) + byte_addr);
-}
-
-// Per-lane LDS base of each slice table: pair * 64 KiB + half * 128 + bank*4.
-// T3 (first byte of a word) -> pair 0 half 0, T2 -> 0/1, T1 -> 1/0, T0 -> 1/1.
-struct SliceBases {
-    uint32_t t3, t2, t1, t0;
-};
-
-__device__ __forceinline__ SliceBases slice_bases(uint32_t lo4)
-{
-    SliceBases b;
-    b.t3 = kLdsS4 + lo4;
-    b.t2 = kLdsS4 + 128u + lo4;
-    b.t1 = kLdsS4 + 65536u + lo4;
-    b.t0 = kLdsS4 + 65536u + 128u + lo4;
-    return b;
-}
-
-// v_perm_b32 builds the LDS address [base.b0 | y.byte_k | base.b2 | 0] in one
-// instruction: row = byte value * 256, column = half*128 + bank*4.
-__device__ __forceinline__ uint32_t tab_addr(uint32_t y, uint32_t base, int k)
-{
-    return __builtin_amdgcn_perm(y, base, 0x0C020400u + ((uint32_t)k << 8));
-}
-
-// One slice-by-4 step: feed the LE word w into raw register c.
-__device__ __forceinline__ uint32_t s4_step(uint32_t c, uint32_t w, const SliceBases &b)
-{
-    const uint32_t y = c ^ w;
-    return lds_read(tab_addr(y, b.t3, 0)) ^ lds_read(tab_addr(y, b.t2, 1)) ^ lds_read(tab_addr(y, b.t1, 2)) ^
-           lds_read(tab_addr(y, b.t0, 3));
-}
-
-// Classic byte step c = T0[(c ^ byte) & 0xff] ^ (c >> 8) (reference val_core.c:157).
-__device__ __forceinline__ uint32_t byte_step(uint32_t c, uint32_t byte, const SliceBases &b)
-{
-    return lds_read(tab_addr(c ^ byte, b.t0, 0)) ^ (c >> 8);
-}
-
-// Advance a register over the (G-1)*UNIT bytes between a lane's units.
-__device__ __forceinline__ uint32_t gap_step(uint32_t a, uint32_t lo4)
-{
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) r ^= lds_read(kLdsGap + (uint32_t)k * 2048u + (((a >> (4 * k)) & 15u) << 7) + lo4);
-    return r;
-}
-
-__device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *col)
-{
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < 32; i++) r ^= (0u - ((v >> i) & 1u)) & col[i];
-    return r;
-}
-
-__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const u32u *>(p); }
-
-template <int G>
-__device__ void build_tables(const FrameParams &p)
-{
-    const int t = threadIdx.x;
-    {   // slice tables: thread t builds T_k[b], k = t>>8, b = t&255, 32 bank replicas
-        const int k = t >> 8, b = t & 255;
-        const uint32_t v = gf2_mul(p.xtab[k], (uint32_t)b);
-        const int slot = 3 - k;  // T3 -> slot 0 ... T0 -> slot 3
-        uint32_t *row = s_lds + (kLdsS4 + (uint32_t)(slot >> 1) * 65536u + (uint32_t)b * 256u + (uint32_t)(slot & 1) * 128u) / 4;
-        const uint4 vv = make_uint4(v, v, v, v);
-#pragma unroll
-        for (int r = 0; r < 8; r++) reinterpret_cast<uint4 *>(row)[r] = vv;
-    }
-    if (G > 1 && t < 128) {  // gap nibble tables: NT_k[n] = gap(n << 4k)
-        const int k = t >> 4, nib = t & 15;
-        const uint32_t v = gf2_mul(p.xgap, (uint32_t)nib << (4 * k));
-        uint32_t *row = s_lds + (kLdsGap + (uint32_t)k * 2048u + (uint32_t)nib * 128u) / 4;
-        const uint4 vv = make_uint4(v, v, v, v);
-#pragma unroll
-        for (int r = 0; r < 8; r++) reinterpret_cast<uint4 *>(row)[r] = vv;
-    }
-    __syncthreads();
-}
-
-// Words of one virtual lane's unit for round 0 (see header comment):
-// u > 0: a full unit of unaligned dwordx4 loads; u == 0: the front-padded
-// first unit, assembled word by word with the seed XORed into frame bytes
-// 0..3; u < 0: nothing (zeros keep a zero register zero). Frames shorter than
-// 4 bytes take the byte path instead (tiny = true).
-template <int UNIT>
-__device__ __forceinline__ void load_unit(uint32_t (&w)[UNIT / 4], int u, const uint8_t *fp, uint32_t L, uint32_t pad,
-                                          uint32_t seed, bool &tiny)
-{
-    tiny = false;
-    if (u > 0) {
-        const uint8_t *up = fp + (uint64_t)u * UNIT - pad;
-#pragma unroll
-        for (int q = 0; q < UNIT / 16; q++) {
-            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
-            w[4 * q + 0] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-        // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
-        if (u == 1 && pad > UNIT - 4) w[0] ^= seed >> (8 * (UNIT - pad));
-    } else if (u == 0 && L >= 4) {
-#pragma unroll
-        for (int i = 0; i < UNIT / 4; i++) {
-            const int q = 4 * i - (int)pad;  // frame offset of this word
-            uint32_t x = 0;
-            if (q >= 0) {
-                x = ld32(fp + q);
-                if (q < 4) x ^= seed >> (8 * q);
-            } else if (q > -4) {
-                x = (ld32(fp) ^ seed) << (8 * (-q));
-            }
-            w[i] = x;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < UNIT / 4; i++) w[i] = 0;
-        tiny = (u == 0);
-    }
-}
-
-template <int CH, int G, int UNIT>
-__device__ __forceinline__ void load_round(uint32_t (&w)[CH][UNIT / 4], const uint8_t *up)
-{
-#pragma unroll
-    for (int c = 0; c < CH; c++) {
-#pragma unroll
-        for (int q = 0; q < UNIT / 16; q++) {
-            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + (uint64_t)G * UNIT * c + 16 * q);
-            w[c][4 * q + 0] = v.x;
-            w[c][4 * q + 1] = v.y;
-            w[c][4 * q + 2] = v.z;
-            w[c][4 * q + 3] = v.w;
-        }
-    }
-}
-
-// K1/K2/K3 fused: per-frame CRC (trailer), optional header_crc and verify.
-// G lanes per frame, CH independent chains per lane -> V = G*CH virtual lanes;
-// virtual lane v = g + G*c owns units v, v+V, v+2V, ... (counted so virtual
-// lane V-1 owns the last unit). UNIT bytes per unit. PF: load the next
-// round's units before hashing the current one (register double buffer).
-template <int G, int CH, int UNIT, bool PF>
-__global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
-{
-    constexpr int V = G * CH;
-    constexpr int W = UNIT / 4;
-    build_tables<V>(p);
-    constexpr int kGroups = 64 / G;
-    const int lane = threadIdx.x & 63;
-    const uint32_t lo4 = (uint32_t)(lane & 31) << 2;
-    const SliceBases sb = slice_bases(lo4);
-    const int g = lane % G;
-    const int grp = lane / G;
-    const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
-
-    for (uint64_t fb = wave * kGroups; fb < p.n; fb += nwaves * kGroups) {
-        const uint64_t f = fb + (uint64_t)grp;
-        const bool active = f < p.n;
-        uint64_t off = 0;
-        uint32_t L = 0;
-        if (active) {
-            if (p.off) {
-                off = p.off[f];
-                L = p.len[f];
-            } else {
-                off = f * p.stride;
-                L = (f + 1 == p.n) ? p.last_len : p.flen;
-            }
-        }
-        const uint8_t *fp = p.base + off;
-        const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
-        const uint32_t U = L ? (L + UNIT - 1) / UNIT : 1u;
-        const uint32_t R = active ? (U + V - 1) / V : 0u;
-        const uint32_t pad = U * UNIT - L;
-        // Steady-state cursor: this lane's chain-0 unit of round 1.
-        const uint8_t *up = fp + ((uint64_t)((int)U - V * (int)R + g) + V) * UNIT - pad;
-        uint32_t nxt[PF ? CH : 1][PF ? W : 1];
-        if (PF && R > 1) load_round<CH, G, UNIT>(reinterpret_cast<uint32_t(&)[CH][W]>(nxt), up);
-        uint32_t acc[CH];
-#pragma unroll
-        for (int c = 0; c < CH; c++) acc[c] = 0;
-        if (R > 0) {
-            // Round 0 is the only one that can hold a virtual lane's unit 0
-            // (front padding, seed, tiny frames) or no unit at all; registers
-            // are still zero, so no gap step. Chains run one after another
-            // here to keep register pressure low.
-#pragma unroll
-            for (int c = 0; c < CH; c++) {
-                uint32_t w[W];
-                bool tiny;
-                load_unit<UNIT>(w, (int)U - V * (int)R + g + G * c, fp, L, pad, seed, tiny);
-                uint32_t a = 0;
-#pragma unroll
-                for (int i = 0; i < W; i++) a = s4_step(a, w[i], sb);
-                if (tiny) {  // L < 4: crc state of the few bytes straight from the seed
-                    a = seed;
-                    for (uint32_t i = 0; i < L; i++) a = byte_step(a, fp[i], sb);
-                }
-                acc[c] = a;
-            }
-        }
-        // Steady state: every virtual lane has a full unit u >= 1 in rounds 1..R-1.
-        for (uint32_t k = 1; k < R; k++, up += (uint64_t)V * UNIT) {
-            uint32_t w[CH][W];
-            if (PF) {
-#pragma unroll
-                for (int c = 0; c < CH; c++)
-#pragma unroll
-                    for (int i = 0; i < W; i++) w[c][i] = nxt[PF ? c : 0][PF ? i : 0];
-                if (k + 1 < R) load_round<CH, G, UNIT>(reinterpret_cast<uint32_t(&)[CH][W]>(nxt), up + (uint64_t)V * UNIT);
-            } else {
-                load_round<CH, G, UNIT>(w, up);
-            }
-            // Seed bytes that did not fit in a unit 0 holding < 4 real bytes
-            // land in the first word of unit 1 (k == 1, virtual lane 0).
-            if (k == 1 && g == 0 && pad > UNIT - 4 && (int)U - V * (int)(R - 1) == 1)
-                w[0][0] ^= seed >> (8 * (UNIT - pad));
-            if (V > 1) {
-#pragma unroll
-                for (int c = 0; c < CH; c++) acc[c] = gap_step(acc[c], lo4);
-            }
-#pragma unroll
-            for (int i = 0; i < W; i++) {
-#pragma unroll
-                for (int c = 0; c < CH; c++) acc[c] = s4_step(acc[c], w[c][i], sb);
-            }
-        }
-        // Merge virtual lanes: level j joins blocks of 2^j virtual lanes, the
-        // left one advanced by UNIT * 2^j bytes. Levels below log2(G) cross
-        // lanes (__shfl_xor); the rest combine the chains inside a lane.
-#pragma unroll
-        for (int j = 0; (1 << j) < G; j++) {
-            const bool right = (g >> j) & 1;
-#pragma unroll
-            for (int c = 0; c < CH; c++) {
-                const uint32_t other = __shfl_xor(acc[c], 1 << j);
-                const uint32_t left = right ? other : acc[c];
-                const uint32_t rgt = right ? acc[c] : other;
-                acc[c] = bitmatrix_apply(left, p.tree[j]) ^ rgt;
-            }
-        }
-        constexpr int kLaneLevels = (G >= 64) ? 6 : (G >= 32) ? 5 : (G >= 16) ? 4 : (G >= 8) ? 3 : (G >= 4) ? 2 : (G >= 2) ? 1 : 0;
-#pragma unroll
-        for (int span = 1, lvl = kLaneLevels; span < CH; span <<= 1, lvl++) {
-#pragma unroll
-            for (int c = 0; c + span < CH; c += 2 * span) acc[c] = bitmatrix_apply(acc[c], p.tree[lvl]) ^ acc[c + span];
-        }
-        const uint32_t total = acc[0];
-        if (active && g == G - 1) {
-            const uint32_t crc = total ^ p.xorout;
-            if (p.out_crc) p.out_crc[f] = crc;
-            if (p.verify) {
-                const bool good = (crc == ld32(fp + L));
-                if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
-                if (!good && p.nbad) atomicAdd(p.nbad, 1u);
-            }
-        }
-        if (active && g == 0 && p.out_hdr) {
-            uint32_t h = seed;
-            if (L >= 8) {
-                h = s4_step(h, ld32(fp), sb);
-                h = s4_step(h, ld32(fp + 4), sb);
-            } else {
-                for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
-            }
-            p.out_hdr[f] = h ^ p.xorout;
-        }
-    }
-}
-
-// Region stage 2: fold per-chunk raw states. Chunks 0..n-2 are `clen` bytes,
-// chunk n-1 is `last_len`. One workgroup, pairwise tree in LDS.
-constexpr int kMaxChunks = 16384;
-struct CombineParams {
-    const uint32_t *states;
-    uint32_t n;
-    uint32_t *out;
-    uint32_t levels;                 // ceil(log2(n-1)) levels of "advance clen*2^j"
-    uint32_t col[15][32];            // level maps
-    uint32_t last_col[32];           // advance last_len bytes
-};
-
-__global__ __launch_bounds__(1024) void k_combine(const CombineParams p)
-{
-    __shared__ uint32_t v[kMaxChunks];
-    const uint32_t m = p.n - 1;                // equal-length chunks
-    const uint32_t P = 1u << p.levels;         // padded to a power of two, zeros in front
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) v[i] = (i >= P - m) ? p.states[i - (P - m)] : 0u;
-    __syncthreads();
-    uint32_t width = P;
-    for (uint32_t lv = 0; lv < p.levels; lv++) {
-        const uint32_t half = width >> 1;
-        uint32_t tmp[kMaxChunks / 2 / 1024 > 0 ? kMaxChunks / 2 / 1024 : 1];
-        int cnt = 0;
-        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) tmp[cnt++] = bitmatrix_apply(v[2 * i], p.col[lv]) ^ v[2 * i + 1];
-        __syncthreads();
-        cnt = 0;
-        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) v[i] = tmp[cnt++];
-        __syncthreads();
-        width = half;
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t head = (m > 0) ? v[0] : 0u;
-        *p.out = bitmatrix_apply(head, p.last_col) ^ p.states[p.n - 1];
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Host side
@@ -451,10 +84,9 @@ val_status_t bind_thread()
 }
 
 bool valid_lanes(uint32_t g) { return g == 1 || g == 2 || g == 4 || g == 8 || g == 16 || g == 32 || g == 64; }
-bool valid_chains(uint32_t c) { return c == 1 || c == 2; }
 
 std::atomic<uint32_t> g_forced_lanes{0};
-std::atomic<uint32_t> g_forced_chains{0};
+std::atomic<int> g_forced_prefetch{-1};
 
 uint32_t env_u32(const char *name)
 {
@@ -462,108 +94,106 @@ uint32_t env_u32(const char *name)
     return e ? (uint32_t)atoi(e) : 0u;
 }
 
-// Lanes that share one frame (G). Short frames share a wave (64/G frames per
-// wave); long frames spread over more lanes so every lane hashes a few KiB.
-uint32_t lanes_per_frame(uint32_t len)
+// Lanes forced by val_gpu_set_lanes_per_frame or VAL_GPU_LANES_PER_FRAME (0 = none).
+uint32_t forced_lanes()
 {
     static const uint32_t env_g = env_u32("VAL_GPU_LANES_PER_FRAME");
     const uint32_t forced = g_forced_lanes.load(std::memory_order_relaxed);
     if (valid_lanes(forced)) return forced;
-    if (valid_lanes(env_g)) return env_g;
-    // Measured on MI355X (tools/sweep_geometry.py): ~2 KiB of CRC input per
-    // lane, at least 4 and at most 32 lanes per frame.
-    uint32_t g = 4;
-    while (g < 32 && (uint64_t)len >= (uint64_t)g * 2u * 2048u) g <<= 1;
-    return g;
+    return valid_lanes(env_g) ? env_g : 0u;
 }
 
-// Independent CRC chains per lane (CH): more loads and LDS lookups in flight.
-uint32_t chains_per_lane(uint32_t len)
+// Lanes that share one frame (G): the length class's measured best.
+uint32_t lanes_per_frame(uint32_t len)
 {
-    static const uint32_t env_c = env_u32("VAL_GPU_CHAINS_PER_LANE");
-    const uint32_t forced = g_forced_chains.load(std::memory_order_relaxed);
-    if (valid_chains(forced)) return forced;
-    if (valid_chains(env_c)) return env_c;
-    (void)len;
-    return 1;
+    const uint32_t f = forced_lanes();
+    return f ? f : (uint32_t)class_lanes(length_class(len));
 }
 
-bool valid_unit(uint32_t u) { return u == 64 || u == 128; }
-std::atomic<uint32_t> g_forced_unit{0};
-std::atomic<int> g_forced_prefetch{-1};
-
-// Bytes a lane hashes per round.
-uint32_t unit_bytes(uint32_t len)
-{
-    static const uint32_t env_u = env_u32("VAL_GPU_UNIT");
-    const uint32_t forced = g_forced_unit.load(std::memory_order_relaxed);
-    if (valid_unit(forced)) return forced;
-    if (valid_unit(env_u)) return env_u;
-    (void)len;
-    return 64;
-}
-
-bool prefetch_on(uint32_t len)
+bool prefetch_on()
 {
     static const int env_p = getenv("VAL_GPU_PREFETCH") ? atoi(getenv("VAL_GPU_PREFETCH")) : -1;
     const int forced = g_forced_prefetch.load(std::memory_order_relaxed);
     if (forced >= 0) return forced != 0;
     if (env_p >= 0) return env_p != 0;
-    (void)len;
     return true;
 }
 
-void fill_geometry(FrameParams &p, uint32_t V, uint32_t unit)
+void fill_constants(FrameParams &p)
 {
     for (int k = 0; k < 4; k++) p.xtab[k] = gf2_x8n((uint64_t)(k + 1));
-    p.xgap = gf2_x8n((uint64_t)(V - 1) * unit);
-    for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)unit << j, p.tree[j]);
-}
-
-template <int G, int UNIT, bool PF>
-void launch_gup(uint32_t CH, dim3 grid, dim3 block, hipStream_t s, const FrameParams &p)
-{
-    if (CH == 2) hipLaunchKernelGGL((k_frames<G, 2, UNIT, PF>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((k_frames<G, 1, UNIT, PF>), grid, block, 0, s, p);
+    for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)kUnit << j, p.tree[j]);
 }
 
 template <int G>
-void launch_g(uint32_t CH, uint32_t unit, bool pf, dim3 grid, dim3 block, hipStream_t s, const FrameParams &p)
+void launch_uniform_g(bool pf, dim3 grid, hipStream_t s, const FrameParams &p)
 {
-    if (unit == 128) {
-        if (pf) launch_gup<G, 128, true>(CH, grid, block, s, p);
-        else launch_gup<G, 128, false>(CH, grid, block, s, p);
-    } else {
-        if (pf) launch_gup<G, 64, true>(CH, grid, block, s, p);
-        else launch_gup<G, 64, false>(CH, grid, block, s, p);
-    }
+    if (pf) hipLaunchKernelGGL((k_frames<G, true>), grid, dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL((k_frames<G, false>), grid, dim3(kBlock), 0, s, p);
 }
 
-val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
+val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
 {
-    if (p.n == 0) return VAL_OK;
-    const uint32_t G = lanes_per_frame(typical_len);
-    const uint32_t CH = chains_per_lane(typical_len);
-    const uint32_t unit = unit_bytes(typical_len);
-    const bool pf = prefetch_on(typical_len);
-    fill_geometry(p, G * CH, unit);
-    const uint64_t groups_per_block = (uint64_t)(kBlock / 64) * (64 / G);
+    fill_constants(p);
+    p.xgap[0] = gf2_x8n((uint64_t)(G - 1) * kUnit);
+    const uint64_t groups_per_block = (uint64_t)kWavesPerBlock * (64 / G);
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
-    blocks = std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus);  // one 144 KiB-LDS workgroup per CU, persistent
-    if (blocks == 0) blocks = 1;
-    dim3 grid((unsigned)blocks), block(kBlock);
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus));  // persistent, 1 per CU (LDS)
+    const dim3 grid((unsigned)blocks);
+    const bool pf = prefetch_on();
     switch (G) {
-    case 1: launch_g<1>(CH, unit, pf, grid, block, s, p); break;
-    case 2: launch_g<2>(CH, unit, pf, grid, block, s, p); break;
-    case 4: launch_g<4>(CH, unit, pf, grid, block, s, p); break;
-    case 8: launch_g<8>(CH, unit, pf, grid, block, s, p); break;
-    case 16: launch_g<16>(CH, unit, pf, grid, block, s, p); break;
-    case 32: launch_g<32>(CH, unit, pf, grid, block, s, p); break;
-    case 64: launch_g<64>(CH, unit, pf, grid, block, s, p); break;
+    case 1: launch_uniform_g<1>(pf, grid, s, p); break;
+    case 2: launch_uniform_g<2>(pf, grid, s, p); break;
+    case 4: launch_uniform_g<4>(pf, grid, s, p); break;
+    case 8: launch_uniform_g<8>(pf, grid, s, p); break;
+    case 16: launch_uniform_g<16>(pf, grid, s, p); break;
+    case 32: launch_uniform_g<32>(pf, grid, s, p); break;
+    case 64: launch_uniform_g<64>(pf, grid, s, p); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
     return VAL_OK;
+}
+
+// Ragged descriptor batch: bin by length class on the device, then one
+// grouped launch planned by bytes per class (no host synchronisation).
+val_status_t launch_ragged(FrameParams &p, hipStream_t s)
+{
+    const uint32_t n = p.n;
+    const uint32_t nbin = std::max(1u, std::min(256u, (n + 255u) / 256u));
+    const uint32_t chunk = (n + nbin - 1) / nbin;
+    const uint32_t nplan = 4u * (uint32_t)g_ctx.cus + kClasses;
+    const size_t sz_hist = (size_t)nbin * kClasses * 4u, sz_hbytes = (size_t)nbin * kClasses * 8u;
+    const size_t sz_base = sz_hist, sz_order = (size_t)n * 4u, sz_plan = (size_t)nplan * 12u;
+    uint8_t *scratch = nullptr;
+    VCRC_HIP(hipMallocAsync((void **)&scratch, sz_hbytes + sz_hist + sz_base + sz_order + sz_plan, s),
+             "hipMallocAsync(bin scratch)");
+    unsigned long long *hbytes = reinterpret_cast<unsigned long long *>(scratch);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(scratch + sz_hbytes);
+    uint32_t *base = hist + (size_t)nbin * kClasses;
+    uint32_t *order = base + (size_t)nbin * kClasses;
+    uint32_t *plan = order + n;
+    hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, hist, hbytes);
+    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, hist, hbytes, nbin, base, plan, nplan);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, base, order);
+    fill_constants(p);
+    for (int c = 0; c < kClasses; c++) p.xgap[c] = gf2_x8n((uint64_t)(class_lanes(c) - 1) * kUnit);
+    p.order = order;
+    p.plan = plan;
+    if (prefetch_on()) hipLaunchKernelGGL(k_frames_grouped<true>, dim3(nplan), dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL(k_frames_grouped<false>, dim3(nplan), dim3(kBlock), 0, s, p);
+    hipError_t e = hipGetLastError();
+    (void)hipFreeAsync(scratch, s);
+    if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
+    return VAL_OK;
+}
+
+// typical_len == 0 with descriptors means "lengths unknown or mixed": bin them.
+val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
+{
+    if (p.n == 0) return VAL_OK;
+    if (p.off && typical_len == 0 && !forced_lanes()) return launch_ragged(p, s);
+    return launch_uniform(p, lanes_per_frame(typical_len ? typical_len : 16384u), s);
 }
 
 // NULL selects the HIP default (null) stream, as in every HIP API.
@@ -785,25 +415,9 @@ val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes)
     return VAL_OK;
 }
 
-uint32_t val_gpu_chains_per_lane(uint32_t typical_len) { return chains_per_lane(typical_len); }
-
-val_status_t val_gpu_set_unit_bytes(uint32_t unit)
-{
-    if (unit != 0 && !valid_unit(unit)) return fail(VAL_ERR_INVALID_ARG, "unit must be 0, 64 or 128");
-    g_forced_unit.store(unit, std::memory_order_relaxed);
-    return VAL_OK;
-}
-
 val_status_t val_gpu_set_prefetch(int on)
 {
     g_forced_prefetch.store(on < 0 ? -1 : (on ? 1 : 0), std::memory_order_relaxed);
-    return VAL_OK;
-}
-
-val_status_t val_gpu_set_chains_per_lane(uint32_t chains)
-{
-    if (chains != 0 && !valid_chains(chains)) return fail(VAL_ERR_INVALID_ARG, "chains must be 0, 1 or 2");
-    g_forced_chains.store(chains, std::memory_order_relaxed);
     return VAL_OK;
 }
 
@@ -854,8 +468,7 @@ val_status_t val_crc32_frames_dev(const uint8_t *d_base, const uint64_t *d_off, 
     p.xorout = 0xFFFFFFFFu;
     p.out_crc = d_crc;
     p.out_hdr = d_hdr;
-    const uint32_t typical = d_off ? (len_hint ? len_hint : 16384u) : flen;
-    return launch_frames(p, typical, pick_stream(stream));
+    return launch_frames(p, d_off ? len_hint : flen, pick_stream(stream));
 }
 
 val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
@@ -882,8 +495,7 @@ val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *
     p.verify = 1;
     p.out_ok = d_ok;
     p.nbad = d_nbad;
-    const uint32_t typical = d_off ? (len_hint ? len_hint : 16384u) : flen;
-    return launch_frames(p, typical, pick_stream(stream));
+    return launch_frames(p, d_off ? len_hint : flen, pick_stream(stream));
 }
 
 val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_state_out,
