@@ -6,7 +6,10 @@
 //   [0, 128 KiB)      slice tables T3|T2 (pair 0) and T1|T0 (pair 1):
 //                     row = byte value * 256 B, half = 128 B, 32 bank replicas
 //                     of 4 B, so the 32 lanes of a half-wave read 32 banks.
-//   [128, 144 KiB)    gap map as 8 nibble tables x 16 rows x 32 replicas.
+//   [128, 160 KiB)    gap maps as 8 nibble tables x 16 rows: one map with 32
+//                     replicas (uniform kernel, 16 KiB) or four maps with 16
+//                     replicas (ragged kernel, 4 x 8 KiB; lanes l and l+16
+//                     share a replica, so a gap lookup is at most 2-way).
 // T_k[b] = b * x^(8(k+1)) mod P (T_0 = the classic table of the reference,
 // src/val_core.c:133-148).
 #pragma once
@@ -24,7 +27,7 @@ constexpr int kBlock = 1024;           // threads per workgroup (16 waves, 1 wor
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kLdsS4 = 0;
 constexpr uint32_t kLdsGap = 131072;
-constexpr uint32_t kLdsWords = (131072 + 16384) / 4;
+constexpr uint32_t kLdsWords = (131072 + 32768) / 4;  // 160 KiB: the whole LDS of a CU
 constexpr int kMaxTree = 6;            // log2(64 lanes)
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -70,12 +73,15 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t c, uint32_t byte, const S
 }
 
 // Advance a register over the bytes other lanes own between two of this
-// lane's units: 8 nibble lookups in the gap tables.
-__device__ __forceinline__ uint32_t gap_step(uint32_t a, uint32_t lo4)
+// lane's units: 8 nibble lookups in a gap map with REPL replicas per row,
+// based at `base` (byte address); lane_off = (lane % REPL) * 4.
+template <int REPL>
+__device__ __forceinline__ uint32_t gap_step(uint32_t a, uint32_t base, uint32_t lane_off)
 {
+    constexpr uint32_t kRow = REPL * 4, kTab = 16 * kRow;
     uint32_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) r ^= lds_read(kLdsGap + (uint32_t)k * 2048u + (((a >> (4 * k)) & 15u) << 7) + lo4);
+    for (int k = 0; k < 8; k++) r ^= lds_read(base + (uint32_t)k * kTab + ((a >> (4 * k)) & 15u) * kRow + lane_off);
     return r;
 }
 
@@ -88,32 +94,36 @@ __device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *
     return r;
 }
 
-// Prologue: slice tables from x^(8(k+1)) (xtab) and, if with_gap, the gap
-// nibble tables of the map "advance by gap bytes" given as x^(8 gap) (xgap).
-__device__ void build_tables(const uint32_t (&xtab)[4], uint32_t xgap, bool with_gap)
+// Prologue, slice tables: T_k from x^(8(k+1)) (xtab), 32 bank replicas.
+__device__ __forceinline__ void build_slice_tables(const uint32_t (&xtab)[4])
+{
+    const int t = threadIdx.x;  // thread t: T_k[b], k = t >> 8, b = t & 255
+    const int k = t >> 8, b = t & 255;
+    // constant indices: a per-thread index would spill the kernel arguments to scratch
+    const uint32_t xk = k == 0 ? xtab[0] : k == 1 ? xtab[1] : k == 2 ? xtab[2] : xtab[3];
+    const uint32_t v = gf2_mul(xk, (uint32_t)b);
+    const int slot = 3 - k;
+    uint4 *row = reinterpret_cast<uint4 *>(
+        s_lds + (kLdsS4 + (uint32_t)(slot >> 1) * 65536u + (uint32_t)b * 256u + (uint32_t)(slot & 1) * 128u) / 4);
+    const uint4 vv = make_uint4(v, v, v, v);
+#pragma unroll
+    for (int r = 0; r < 8; r++) row[r] = vv;
+}
+
+// Prologue, one gap map "advance by gap bytes" (xgap = x^(8 gap)) at `base`
+// with REPL replicas: threads 0..127 each build one (table, nibble) row.
+template <int REPL>
+__device__ __forceinline__ void build_gap_table(uint32_t xgap, uint32_t base)
 {
     const int t = threadIdx.x;
-    {   // thread t: T_k[b], k = t >> 8, b = t & 255, written to its 32 replicas
-        const int k = t >> 8, b = t & 255;
-        // constant indices: a per-thread index would spill the kernel arguments to scratch
-        const uint32_t xk = k == 0 ? xtab[0] : k == 1 ? xtab[1] : k == 2 ? xtab[2] : xtab[3];
-        const uint32_t v = gf2_mul(xk, (uint32_t)b);
-        const int slot = 3 - k;
-        uint4 *row = reinterpret_cast<uint4 *>(
-            s_lds + (kLdsS4 + (uint32_t)(slot >> 1) * 65536u + (uint32_t)b * 256u + (uint32_t)(slot & 1) * 128u) / 4);
-        const uint4 vv = make_uint4(v, v, v, v);
-#pragma unroll
-        for (int r = 0; r < 8; r++) row[r] = vv;
-    }
-    if (with_gap && t < 128) {  // NT_k[n] = gap(n << 4k)
+    if (t < 128) {  // NT_k[n] = gap(n << 4k)
         const int k = t >> 4, nib = t & 15;
         const uint32_t v = gf2_mul(xgap, (uint32_t)nib << (4 * k));
-        uint4 *row = reinterpret_cast<uint4 *>(s_lds + (kLdsGap + (uint32_t)k * 2048u + (uint32_t)nib * 128u) / 4);
+        uint4 *row = reinterpret_cast<uint4 *>(s_lds + (base + (uint32_t)k * (16u * REPL * 4u) + (uint32_t)nib * (REPL * 4u)) / 4);
         const uint4 vv = make_uint4(v, v, v, v);
 #pragma unroll
-        for (int r = 0; r < 8; r++) row[r] = vv;
+        for (int r = 0; r < REPL / 4; r++) row[r] = vv;
     }
-    __syncthreads();
 }
 
 }  // namespace vcrc

@@ -2,11 +2,12 @@
 //
 // k_frames<G, PF>      K1/K2/K3: per-frame trailer CRC, header_crc, verify;
 //                      persistent grid, G lanes per frame, uniform geometry.
-// k_bin_* + k_frames_grouped<PF>
-//                      K5: ragged descriptor batches. Frames are binned by
-//                      length class on the device (stable), each class gets its
-//                      measured lanes-per-frame, and workgroups are planned in
-//                      proportion to each class's bytes. No host round trip.
+// k_bin_* + k_frames_ragged<PF>
+//                      K5: ragged descriptor batches. Frames are counting-
+//                      sorted by length on the device (512-B buckets, longest
+//                      first), each length class runs its measured lanes per
+//                      frame; a persistent grid walks the sorted items
+//                      longest first. No host round trip.
 // k_combine            K4 stage 2: fold per-chunk raw states of a long region.
 //
 // Frame algorithm (all GF(2)-linear):
@@ -50,11 +51,35 @@ struct FrameParams {
     uint32_t *nbad;
     uint32_t verify;
     const uint32_t *order;   // grouped mode: class-sorted frame indices
-    const uint32_t *plan;    // grouped mode: {class, begin, end} per workgroup
+    const uint32_t *plan;    // ragged mode: class table {cstart[4], ccount[4], istart[5]}
     uint32_t xtab[4];        // x^(8(k+1)): slice table T_k
     uint32_t xgap[kClasses]; // x^(8 (G-1) 64) per geometry (index 0 in uniform mode)
     uint32_t tree[kMaxTree][32];  // columns of "advance 64 * 2^j bytes"
 };
+
+// A full 64-B unit starting at byte address up, read with dword-aligned
+// loads only: 4 dwordx4 from floor4(up) plus one dword when up is not
+// 4-aligned (b = up & 3 = the same for every unit of a frame), then each word
+// funnel-shifted into place with v_alignbyte_b32. A dword-aligned load never
+// crosses a page, and device allocations are at least 4-aligned, so nothing
+// outside the buffer's pages is touched. Byte-misaligned dwordx4 loads would
+// cost ~60% of the ragged path's throughput (profiles/r01_ragged_pmc.txt).
+__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up, uint32_t b)
+{
+    const uint8_t *a = up - b;
+    uint32_t d[kWords + 1];
+#pragma unroll
+    for (int q = 0; q < kWords / 4; q++) {
+        const u32x4u v = *reinterpret_cast<const u32x4u *>(a + 16 * q);
+        d[4 * q + 0] = v.x;
+        d[4 * q + 1] = v.y;
+        d[4 * q + 2] = v.z;
+        d[4 * q + 3] = v.w;
+    }
+    d[kWords] = b ? *reinterpret_cast<const uint32_t *>(a + kUnit) : 0u;
+#pragma unroll
+    for (int i = 0; i < kWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], b);
+}
 
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
 // first unit, assembled word by word with the seed in frame bytes 0..3;
@@ -65,14 +90,7 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const u
     tiny = false;
     if (u > 0) {
         const uint8_t *up = fp + (uint64_t)u * kUnit - pad;
-#pragma unroll
-        for (int q = 0; q < kWords / 4; q++) {
-            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
-            w[4 * q + 0] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
+        load_full(w, up, (uint32_t)(uintptr_t)up & 3u);
         // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
         if (u == 1 && pad > kUnit - 4) w[0] ^= seed >> (8 * (kUnit - pad));
     } else if (u == 0 && L >= 4) {
@@ -95,35 +113,25 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const u
     }
 }
 
-__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up)
+// Descriptor of frame f (offset and CRC-input length).
+__device__ __forceinline__ void frame_desc(const FrameParams &p, uint64_t f, uint64_t &off, uint32_t &L)
 {
-#pragma unroll
-    for (int q = 0; q < kWords / 4; q++) {
-        const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
-        w[4 * q + 0] = v.x;
-        w[4 * q + 1] = v.y;
-        w[4 * q + 2] = v.z;
-        w[4 * q + 3] = v.w;
+    if (p.off) {
+        off = p.off[f];
+        L = p.len[f];
+    } else {
+        off = f * p.stride;
+        L = (f + 1 == p.n) ? p.last_len : p.flen;
     }
 }
 
-// Hash frame f with the G lanes of this lane's group (g = 0..G-1). All 64
-// lanes of the wave must call this together (the merge tree shuffles).
-template <int G, bool PF>
-__device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, int g, uint32_t lo4,
-                                           const SliceBases &sb)
+// Hash frame f (at base + off, L bytes) with the G lanes of this lane's group
+// (g = 0..G-1). All 64 lanes of the wave must call this together (the merge
+// tree shuffles); inactive lanes pass L = 0.
+template <int G, bool PF, int REPL>
+__device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
+                                           uint32_t gap_base, uint32_t gap_lane, const SliceBases &sb)
 {
-    uint64_t off = 0;
-    uint32_t L = 0;
-    if (active) {
-        if (p.off) {
-            off = p.off[f];
-            L = p.len[f];
-        } else {
-            off = f * p.stride;
-            L = (f + 1 == p.n) ? p.last_len : p.flen;
-        }
-    }
     const uint8_t *fp = p.base + off;
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
     const uint32_t U = L ? (L + kUnit - 1) / kUnit : 1u;
@@ -131,8 +139,9 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     const uint32_t pad = U * kUnit - L;
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
     const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
+    const uint32_t b = (uint32_t)(uintptr_t)up & 3u;           // same for every unit of the frame
     uint32_t nxt[kWords];
-    if (PF && R > 1) load_full(nxt, up);
+    if (PF && R > 1) load_full(nxt, up, b);
     uint32_t acc = 0;
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
@@ -153,13 +162,13 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
         if (PF) {
 #pragma unroll
             for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-            if (k + 1 < R) load_full(nxt, up + (uint64_t)G * kUnit);
+            if (k + 1 < R) load_full(nxt, up + (uint64_t)G * kUnit, b);
         } else {
-            load_full(w, up);
+            load_full(w, up, b);
         }
         // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, k == 1).
         if (k == 1 && g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1) w[0] ^= seed >> (8 * (kUnit - pad));
-        if (G > 1) acc = gap_step(acc, lo4);
+        if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
 #pragma unroll
         for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
     }
@@ -195,174 +204,209 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 template <int G, bool PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
-    build_tables(p.xtab, p.xgap[0], G > 1);
+    build_slice_tables(p.xtab);
+    if (G > 1) build_gap_table<32>(p.xgap[0], kLdsGap);
+    __syncthreads();
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const uint32_t lo4 = (uint32_t)(lane & 31) << 2;
     const SliceBases sb = slice_bases(lo4);
     const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
-    for (uint64_t fb = wave * kGroups; fb < p.n; fb += nwaves * kGroups) {
-        const uint64_t f = fb + (uint64_t)(lane / G);
-        hash_frame<G, PF>(p, f, f < p.n, lane % G, lo4, sb);
+    // Descriptors of the next frame group are fetched while this one hashes.
+    uint64_t fb = wave * kGroups, f = fb + (uint64_t)(lane / G), off = 0;
+    uint32_t L = 0;
+    if (f < p.n) frame_desc(p, f, off, L);
+    for (; fb < p.n; fb += nwaves * kGroups) {
+        const uint64_t fn = f + nwaves * kGroups;
+        uint64_t off_n = 0;
+        uint32_t L_n = 0;
+        if (fn < p.n) frame_desc(p, fn, off_n, L_n);
+        hash_frame<G, PF, 32>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
+        f = fn;
+        off = off_n;
+        L = L_n;
     }
 }
 
 // ---- ragged path ------------------------------------------------------------
-// Pass 1: per-workgroup counts and bytes of each length class.
-__global__ __launch_bounds__(256) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk, uint32_t *hist,
-                                                   unsigned long long *hbytes)
+// Frames are counting-sorted by length bucket (512 B wide, longest first) so
+// the 64/G frames a wave hashes together have nearly equal lengths, and the
+// sorted order is cut into geometry classes (contiguous bucket ranges).
+constexpr int kBucketBytes = 512;
+constexpr int kBuckets = 129;  // [0,512), ..., [65024,65536), [65536, inf)
+__host__ __device__ inline int length_bucket(uint32_t L)
 {
-    __shared__ uint32_t cnt[kClasses];
-    __shared__ unsigned long long bytes[kClasses];
-    if (threadIdx.x < kClasses) {
-        cnt[threadIdx.x] = 0;
-        bytes[threadIdx.x] = 0;
+    const uint32_t b = L / kBucketBytes;
+    return b < (uint32_t)(kBuckets - 1) ? (int)b : kBuckets - 1;
+}
+// Sorted position of a bucket: longest bucket first.
+__host__ __device__ inline int bucket_rank(int b) { return kBuckets - 1 - b; }
+__host__ __device__ inline int bucket_class(int b) { return length_class((uint32_t)b * kBucketBytes); }
+
+// Pass 1: per-workgroup bucket counts; each workgroup reserves its slice of
+// every non-empty bucket with one atomic (offsets within the bucket) and adds
+// the bucket's bytes. gcount/gbytes must be zero on entry.
+__global__ __launch_bounds__(256) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk, uint32_t *gcount,
+                                                   unsigned long long *gbytes, uint32_t *blockoff)
+{
+    __shared__ uint32_t cnt[kBuckets];
+    __shared__ unsigned long long bytes[kBuckets];
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) {
+        cnt[b] = 0;
+        bytes[b] = 0;
     }
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
     for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         const uint32_t L = len[i];
-        const int c = length_class(L);
-        atomicAdd(&cnt[c], 1u);
-        atomicAdd(&bytes[c], (unsigned long long)L);
+        const int b = length_bucket(L);
+        atomicAdd(&cnt[b], 1u);
+        atomicAdd(&bytes[b], (unsigned long long)L);
     }
     __syncthreads();
-    if (threadIdx.x < kClasses) {
-        hist[blockIdx.x * kClasses + threadIdx.x] = cnt[threadIdx.x];
-        hbytes[blockIdx.x * kClasses + threadIdx.x] = bytes[threadIdx.x];
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) {
+        uint32_t off = 0;
+        if (cnt[b]) {
+            off = atomicAdd(&gcount[b], cnt[b]);
+            atomicAdd(&gbytes[b], bytes[b]);
+        }
+        blockoff[(size_t)blockIdx.x * kBuckets + b] = off;
     }
 }
 
-// Pass 2 (one workgroup): class starts, per-(block, class) scatter bases and
-// the workgroup plan {class, begin, end} (workgroups per class in proportion
-// to its bytes, >= 1 for a non-empty class; unused plan entries are empty).
-__global__ __launch_bounds__(64) void k_bin_plan(const uint32_t *hist, const unsigned long long *hbytes, uint32_t nbin,
-                                                 uint32_t *base, uint32_t *plan, uint32_t nplan)
+// Pass 2 (one workgroup): bucket starts in sorted order (longest first) and
+// the class table: class c occupies sorted positions [cstart, cstart+ccount)
+// and is cut into items of 64/G_c frames (one wave step each); items are
+// numbered longest class first: class c owns items [istart[c], istart[c+1]).
+// ctab = {cstart[4], ccount[4], istart[5]}.
+__global__ __launch_bounds__(256) void k_bin_plan(const uint32_t *gcount, const unsigned long long *gbytes,
+                                                  uint32_t *bstart, uint32_t *ctab)
 {
-    __shared__ uint32_t count[kClasses], start[kClasses], nblk[kClasses];
-    __shared__ unsigned long long cbytes[kClasses];
-    const int c = threadIdx.x;
-    if (c < kClasses) {
-        uint32_t s = 0;
-        unsigned long long b = 0;
-        for (uint32_t k = 0; k < nbin; k++) {
-            base[k * kClasses + c] = s;  // relative to the class start, fixed below
-            s += hist[k * kClasses + c];
-            b += hbytes[k * kClasses + c];
-        }
-        count[c] = s;
-        cbytes[c] = b;
-    }
+    __shared__ uint32_t cnt[kBuckets];
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cnt[b] = gcount[b];
     __syncthreads();
-    if (c == 0) {
-        unsigned long long total = 0;
-        uint32_t s = 0;
-        for (int k = 0; k < kClasses; k++) {
-            start[k] = s;
-            s += count[k];
-            total += cbytes[k];
-        }
-        const uint32_t budget = nplan - kClasses;  // room for the ">= 1" rounding
-        for (int k = 0; k < kClasses; k++) {
-            uint32_t nb = 0;
-            if (count[k]) {
-                nb = total ? (uint32_t)((double)budget * (double)cbytes[k] / (double)total) : 1u;
-                if (nb < 1) nb = 1;
-                if (nb > count[k]) nb = count[k];
-            }
-            nblk[k] = nb;
-        }
+    if (threadIdx.x != 0) return;
+    (void)gbytes;
+    uint32_t ccount[kClasses] = {}, cstart[kClasses];
+    for (int c = 0; c < kClasses; c++) cstart[c] = 0xFFFFFFFFu;
+    uint32_t pos = 0;
+    for (int r = 0; r < kBuckets; r++) {  // longest bucket first
+        const int b = kBuckets - 1 - r, c = bucket_class(b);
+        bstart[b] = pos;
+        if (cnt[b] && pos < cstart[c]) cstart[c] = pos;
+        ccount[c] += cnt[b];
+        pos += cnt[b];
     }
-    __syncthreads();
-    if (c < kClasses) {
-        for (uint32_t k = 0; k < nbin; k++) base[k * kClasses + c] += start[c];
-        uint32_t first = 0;
-        for (int k = 0; k < c; k++) first += nblk[k];
-        for (uint32_t b = 0; b < nblk[c]; b++) {
-            plan[3 * (first + b) + 0] = (uint32_t)c;
-            plan[3 * (first + b) + 1] = start[c] + (uint32_t)((uint64_t)count[c] * b / nblk[c]);
-            plan[3 * (first + b) + 2] = start[c] + (uint32_t)((uint64_t)count[c] * (b + 1) / nblk[c]);
-        }
-        if (c == kClasses - 1) {
-            for (uint32_t b = first + nblk[c]; b < nplan; b++) {
-                plan[3 * b + 0] = 0;
-                plan[3 * b + 1] = 0;
-                plan[3 * b + 2] = 0;
-            }
-        }
+    uint32_t item = 0;
+    for (int c = kClasses - 1; c >= 0; c--) {
+        const uint32_t per = 64u / (uint32_t)class_lanes(c);
+        ctab[8 + c] = item;
+        item += (ccount[c] + per - 1) / per;
+        ctab[c] = ccount[c] ? cstart[c] : 0u;
+        ctab[4 + c] = ccount[c];
     }
+    ctab[12] = item;  // total items
 }
 
-// Pass 3: stable scatter of frame indices into class order.
+// Pass 3: scatter frame indices into sorted order (order within a bucket is
+// unspecified; every output is written at its frame's own index).
 __global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32_t n, uint32_t chunk,
-                                                     const uint32_t *base, uint32_t *order)
+                                                     const uint32_t *bstart, const uint32_t *blockoff, uint32_t *order)
 {
-    __shared__ uint32_t wave_cnt[4][kClasses];
-    __shared__ uint32_t run[kClasses];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x < kClasses) run[threadIdx.x] = base[blockIdx.x * kClasses + threadIdx.x];
+    __shared__ uint32_t cur[kBuckets];
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
+        cur[b] = bstart[b] + blockoff[(size_t)blockIdx.x * kBuckets + b];
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
-    for (uint64_t t0 = lo; t0 < hi; t0 += blockDim.x) {
-        const uint64_t i = t0 + threadIdx.x;
-        const bool valid = i < hi;
-        const int c = valid ? length_class(len[i]) : -1;
-        uint32_t rank = 0;
-#pragma unroll
-        for (int k = 0; k < kClasses; k++) {
-            const unsigned long long m = __ballot(c == k);
-            if (c == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (lane == 0) wave_cnt[wv][k] = (uint32_t)__popcll(m);
-        }
-        __syncthreads();
-        if (valid) {
-            uint32_t before = run[c];
-            for (int w = 0; w < wv; w++) before += wave_cnt[w][c];
-            order[before + rank] = (uint32_t)i;
-        }
-        __syncthreads();
-        if (threadIdx.x < kClasses) {
-            uint32_t add = 0;
-            for (int w = 0; w < 4; w++) add += wave_cnt[w][threadIdx.x];
-            run[threadIdx.x] += add;
-        }
-        __syncthreads();
-    }
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) order[atomicAdd(&cur[length_bucket(len[i])], 1u)] = (uint32_t)i;
 }
 
-template <int G, bool PF>
-__device__ __forceinline__ void hash_range(const FrameParams &p, uint32_t begin, uint32_t end, uint32_t lo4,
+// Item `it` of the ragged plan: its class and sorted-order range.
+struct Item {
+    int c;
+    uint32_t first, end;
+};
+
+__device__ __forceinline__ Item ragged_item(const uint32_t *ctab, uint32_t it)
+{
+    // items are numbered class 3 (longest) first
+    const int c = it >= ctab[8 + 2] ? (it >= ctab[8 + 1] ? (it >= ctab[8 + 0] ? 0 : 1) : 2) : 3;
+    const uint32_t per = 64u / (uint32_t)(c == 0 ? class_lanes(0) : c == 1 ? class_lanes(1) : c == 2 ? class_lanes(2) : class_lanes(3));
+    const uint32_t cstart = c == 0 ? ctab[0] : c == 1 ? ctab[1] : c == 2 ? ctab[2] : ctab[3];
+    const uint32_t ccount = c == 0 ? ctab[4] : c == 1 ? ctab[5] : c == 2 ? ctab[6] : ctab[7];
+    const uint32_t istart = c == 0 ? ctab[8] : c == 1 ? ctab[9] : c == 2 ? ctab[10] : ctab[11];
+    return Item{c, cstart + (it - istart) * per, cstart + ccount};
+}
+
+// This lane's frame of an item (lane / G-th frame) and its descriptor.
+__device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, int lane, uint64_t &f, bool &active,
+                                           uint64_t &off, uint32_t &L)
+{
+    const int G = class_lanes(t.c == 0 ? 0 : t.c == 1 ? 1 : t.c == 2 ? 2 : 3);
+    const uint32_t i = t.first + (uint32_t)(lane / G);
+    active = i < t.end;
+    f = active ? p.order[i] : 0u;
+    off = 0;
+    L = 0;
+    if (active) frame_desc(p, f, off, L);
+}
+
+template <int C, bool PF>
+__device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L,
                                            const SliceBases &sb)
 {
-    constexpr int kGroups = 64 / G;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (uint32_t i0 = begin + (uint32_t)wv * kGroups; i0 < end; i0 += (uint32_t)kWavesPerBlock * kGroups) {
-        const uint32_t i = i0 + (uint32_t)(lane / G);
-        const bool active = i < end;
-        const uint64_t f = active ? p.order[i] : 0u;
-        hash_frame<G, PF>(p, f, active, lane % G, lo4, sb);
-    }
+    constexpr int G = class_lanes(C);
+    const int lane = threadIdx.x & 63;
+    hash_frame<G, PF, 16>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
 }
 
-// Ragged batches: workgroup b hashes the class-sorted frames plan[b] with the
-// class's lanes per frame.
+// Ragged batches: persistent grid; every wave walks the items (64/G frames of
+// one class, longest first) cyclically, fetching the next item's descriptors
+// while it hashes the current one. All four classes' gap maps stay in LDS, so
+// waves never synchronise after the prologue.
 template <bool PF>
-__global__ __launch_bounds__(kBlock) void k_frames_grouped(const FrameParams p)
+__global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
-    const uint32_t cls = p.plan[3 * blockIdx.x], begin = p.plan[3 * blockIdx.x + 1], end = p.plan[3 * blockIdx.x + 2];
-    if (begin >= end) return;
-    // Constant indices only: a runtime index into the kernel arguments would
-    // copy them to scratch.
-    const uint32_t xgap = cls == 0 ? p.xgap[0] : cls == 1 ? p.xgap[1] : cls == 2 ? p.xgap[2] : p.xgap[3];
-    build_tables(p.xtab, xgap, true);
-    const uint32_t lo4 = (uint32_t)(threadIdx.x & 31) << 2;
-    const SliceBases sb = slice_bases(lo4);
-    switch (cls) {
-    case 0: hash_range<class_lanes(0), PF>(p, begin, end, lo4, sb); break;
-    case 1: hash_range<class_lanes(1), PF>(p, begin, end, lo4, sb); break;
-    case 2: hash_range<class_lanes(2), PF>(p, begin, end, lo4, sb); break;
-    default: hash_range<class_lanes(3), PF>(p, begin, end, lo4, sb); break;
+    build_slice_tables(p.xtab);
+    build_gap_table<16>(p.xgap[0], kLdsGap + 0u * 8192u);
+    build_gap_table<16>(p.xgap[1], kLdsGap + 1u * 8192u);
+    build_gap_table<16>(p.xgap[2], kLdsGap + 2u * 8192u);
+    build_gap_table<16>(p.xgap[3], kLdsGap + 3u * 8192u);
+    __syncthreads();
+    const uint32_t *ctab = p.plan;
+    const uint32_t items = ctab[12];
+    const int lane = threadIdx.x & 63;
+    const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
+    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
+    uint32_t it = wave;
+    if (it >= items) return;
+    Item cur = ragged_item(ctab, it);
+    uint64_t f, off;
+    uint32_t L;
+    bool active;
+    item_frame(p, cur, lane, f, active, off, L);
+    for (; it < items; it += nwaves) {
+        Item nxt{0, 0, 0};
+        uint64_t f_n = 0, off_n = 0;
+        uint32_t L_n = 0;
+        bool active_n = false;
+        if (it + nwaves < items) {
+            nxt = ragged_item(ctab, it + nwaves);
+            item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
+        }
+        switch (cur.c) {
+        case 3: hash_class<3, PF>(p, f, active, off, L, sb); break;
+        case 2: hash_class<2, PF>(p, f, active, off, L, sb); break;
+        case 1: hash_class<1, PF>(p, f, active, off, L, sb); break;
+        default: hash_class<0, PF>(p, f, active, off, L, sb); break;
+        }
+        cur = nxt;
+        f = f_n;
+        off = off_n;
+        L = L_n;
+        active = active_n;
     }
 }
 

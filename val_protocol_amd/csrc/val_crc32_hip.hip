@@ -155,34 +155,43 @@ val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
     return VAL_OK;
 }
 
-// Ragged descriptor batch: bin by length class on the device, then one
-// grouped launch planned by bytes per class (no host synchronisation).
+// Ragged descriptor batch: counting-sort by length on the device, then one
+// grouped launch planned by bytes per length class (no host synchronisation).
 val_status_t launch_ragged(FrameParams &p, hipStream_t s)
 {
     const uint32_t n = p.n;
-    const uint32_t nbin = std::max(1u, std::min(256u, (n + 255u) / 256u));
+    const uint32_t nbin = std::max(1u, std::min(64u, (n + 1023u) / 1024u));
     const uint32_t chunk = (n + nbin - 1) / nbin;
-    const uint32_t nplan = 4u * (uint32_t)g_ctx.cus + kClasses;
-    const size_t sz_hist = (size_t)nbin * kClasses * 4u, sz_hbytes = (size_t)nbin * kClasses * 8u;
-    const size_t sz_base = sz_hist, sz_order = (size_t)n * 4u, sz_plan = (size_t)nplan * 12u;
+    // scratch: gbytes[kBuckets] u64 | gcount[kBuckets] u32 | bstart[kBuckets] u32 |
+    //          ctab[16] u32 | blockoff[nbin][kBuckets] u32 | order[n] u32
+    const size_t sz_gbytes = (size_t)kBuckets * 8u, sz_gcount = (size_t)kBuckets * 4u;
+    const size_t sz_zero = sz_gbytes + sz_gcount;
+    const size_t total = sz_zero + sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     uint8_t *scratch = nullptr;
-    VCRC_HIP(hipMallocAsync((void **)&scratch, sz_hbytes + sz_hist + sz_base + sz_order + sz_plan, s),
-             "hipMallocAsync(bin scratch)");
-    unsigned long long *hbytes = reinterpret_cast<unsigned long long *>(scratch);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(scratch + sz_hbytes);
-    uint32_t *base = hist + (size_t)nbin * kClasses;
-    uint32_t *order = base + (size_t)nbin * kClasses;
-    uint32_t *plan = order + n;
-    hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, hist, hbytes);
-    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, hist, hbytes, nbin, base, plan, nplan);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, base, order);
-    fill_constants(p);
-    for (int c = 0; c < kClasses; c++) p.xgap[c] = gf2_x8n((uint64_t)(class_lanes(c) - 1) * kUnit);
-    p.order = order;
-    p.plan = plan;
-    if (prefetch_on()) hipLaunchKernelGGL(k_frames_grouped<true>, dim3(nplan), dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL(k_frames_grouped<false>, dim3(nplan), dim3(kBlock), 0, s, p);
-    hipError_t e = hipGetLastError();
+    VCRC_HIP(hipMallocAsync((void **)&scratch, total, s), "hipMallocAsync(bin scratch)");
+    unsigned long long *gbytes = reinterpret_cast<unsigned long long *>(scratch);
+    uint32_t *gcount = reinterpret_cast<uint32_t *>(scratch + sz_gbytes);
+    uint32_t *bstart = gcount + kBuckets;
+    uint32_t *ctab = bstart + kBuckets;
+    uint32_t *blockoff = ctab + 16;
+    uint32_t *order = blockoff + (size_t)nbin * kBuckets;
+    hipError_t e = hipMemsetAsync(scratch, 0, sz_zero, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, gcount, gbytes, blockoff);
+        hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(256), 0, s, gcount, gbytes, bstart, ctab);
+        hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, bstart, blockoff, order);
+        fill_constants(p);
+        for (int c = 0; c < kClasses; c++) p.xgap[c] = gf2_x8n((uint64_t)(class_lanes(c) - 1) * kUnit);
+        p.order = order;
+        p.plan = ctab;
+        // persistent: enough waves for the items, at most one workgroup per CU
+        const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
+        const unsigned blocks = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>((uint64_t)g_ctx.cus, (max_items + kWavesPerBlock - 1) / kWavesPerBlock));
+        if (prefetch_on()) hipLaunchKernelGGL(k_frames_ragged<true>, dim3(blocks), dim3(kBlock), 0, s, p);
+        else hipLaunchKernelGGL(k_frames_ragged<false>, dim3(blocks), dim3(kBlock), 0, s, p);
+        e = hipGetLastError();
+    }
     (void)hipFreeAsync(scratch, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
     return VAL_OK;
