@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""A/B two builds of libval_crc_hip.so in one process on the same inputs:
+interleaved timing of val_crc32_frames_dev (tooling only, not the product).
+usage: ab_libs.py LIB_A LIB_B [cfg3|cfg5|u57]..."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import val_protocol_amd.crc as vc  # noqa: E402
+from tools.sweep_geometry import time_it  # noqa: E402
+
+
+def load(path):
+    l = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
+    vc._declare(l)
+    return l
+
+
+def workload(name, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    if name == "cfg3":
+        n, L = 1 << 20, 16384 - 4
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    rng = np.random.default_rng(1)
+    if name == "cfg5":
+        lens = rng.integers(520, 65533, 262144)
+    elif name == "u57":
+        lens = np.full(56508, 57000)
+    else:
+        raise SystemExit(name)
+    wire = lens + 4
+    off = np.concatenate([[0], np.cumsum(wire)[:-1]])
+    buf = torch.randint(0, 256, (int(wire.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    return dict(buf=buf, off=torch.from_numpy(off.astype(np.int64)).to(dev),
+                length=torch.from_numpy(lens.astype(np.int32)).to(dev), len_hint=0), int(lens.sum())
+
+
+def main():
+    dev = torch.device("cuda:0")
+    libs = [load(sys.argv[1]), load(sys.argv[2])]
+    for l in libs:
+        assert l.val_gpu_init(0) == 0
+    for name in sys.argv[3:] or ["cfg3", "cfg5"]:
+        w, nbytes = workload(name, dev)
+        outs = []
+        res = [[], []]
+        for rep in range(4):
+            for i, l in enumerate(libs):
+                vc._lib = l
+                out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
+                if "off" in w:
+                    fn = lambda: vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=0)
+                else:
+                    fn = lambda: vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
+                med, _ = time_it(fn, reps=10)
+                res[i].append(med)
+                if rep == 0:
+                    outs.append(out.clone())
+        same = bool(torch.equal(outs[0], outs[1]))
+        a, b = np.median(res[0]), np.median(res[1])
+        print(f"{name}: A {a:.4f} ms ({nbytes / a / 1e6:.0f} GB/s)  B {b:.4f} ms ({nbytes / b / 1e6:.0f} GB/s)  "
+              f"B/A speed {a / b:.3f}  same={same}  A={['%.3f' % x for x in res[0]]} B={['%.3f' % x for x in res[1]]}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

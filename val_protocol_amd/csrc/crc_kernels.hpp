@@ -64,8 +64,20 @@ struct FrameParams {
 // crosses a page, and device allocations are at least 4-aligned, so nothing
 // outside the buffer's pages is touched. Byte-misaligned dwordx4 loads would
 // cost ~60% of the ragged path's throughput (profiles/r01_ragged_pmc.txt).
+template <bool ALIGNED>
 __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up, uint32_t b)
 {
+    if (ALIGNED) {  // the host proved every unit dword-aligned (b == 0): plain loads
+#pragma unroll
+        for (int q = 0; q < kWords / 4; q++) {
+            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
+            w[4 * q + 0] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+        return;
+    }
     const uint8_t *a = up - b;
     uint32_t d[kWords + 1];
 #pragma unroll
@@ -84,13 +96,14 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
 // first unit, assembled word by word with the seed in frame bytes 0..3;
 // u < 0 nothing. L < 4 frames take the byte path (tiny).
+template <bool ALIGNED>
 __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const uint8_t *fp, uint32_t L, uint32_t pad,
                                            uint32_t seed, bool &tiny)
 {
     tiny = false;
     if (u > 0) {
         const uint8_t *up = fp + (uint64_t)u * kUnit - pad;
-        load_full(w, up, (uint32_t)(uintptr_t)up & 3u);
+        load_full<ALIGNED>(w, up, (uint32_t)(uintptr_t)up & 3u);
         // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
         if (u == 1 && pad > kUnit - 4) w[0] ^= seed >> (8 * (kUnit - pad));
     } else if (u == 0 && L >= 4) {
@@ -128,7 +141,7 @@ __device__ __forceinline__ void frame_desc(const FrameParams &p, uint64_t f, uin
 // Hash frame f (at base + off, L bytes) with the G lanes of this lane's group
 // (g = 0..G-1). All 64 lanes of the wave must call this together (the merge
 // tree shuffles); inactive lanes pass L = 0.
-template <int G, bool PF, int REPL>
+template <int G, bool PF, int REPL, bool ALIGNED>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            uint32_t gap_base, uint32_t gap_lane, const SliceBases &sb)
 {
@@ -141,14 +154,14 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
     const uint32_t b = (uint32_t)(uintptr_t)up & 3u;           // same for every unit of the frame
     uint32_t nxt[kWords];
-    if (PF && R > 1) load_full(nxt, up, b);
+    if (PF && R > 1) load_full<ALIGNED>(nxt, up, b);
     uint32_t acc = 0;
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
         uint32_t w[kWords];
         bool tiny;
-        load_unit0(w, u0, fp, L, pad, seed, tiny);
+        load_unit0<ALIGNED>(w, u0, fp, L, pad, seed, tiny);
 #pragma unroll
         for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
         if (tiny) {  // L < 4: state of the few bytes straight from the seed
@@ -156,15 +169,14 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
         }
     }
-    // Steady state: every lane has a full unit (u >= 1) in rounds 1..R-1.
     for (uint32_t k = 1; k < R; k++, up += (uint64_t)G * kUnit) {
         uint32_t w[kWords];
         if (PF) {
 #pragma unroll
             for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-            if (k + 1 < R) load_full(nxt, up + (uint64_t)G * kUnit, b);
+            if (k + 1 < R) load_full<ALIGNED>(nxt, up + (uint64_t)G * kUnit, b);
         } else {
-            load_full(w, up, b);
+            load_full<ALIGNED>(w, up, b);
         }
         // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, k == 1).
         if (k == 1 && g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1) w[0] ^= seed >> (8 * (kUnit - pad));
@@ -201,7 +213,8 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 }
 
 // Uniform geometry: persistent grid, each wave hashes 64/G frames per step.
-template <int G, bool PF>
+// ALIGNED: the host proved every unit start dword-aligned (strided batches).
+template <int G, bool PF, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
     build_slice_tables(p.xtab);
@@ -222,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         uint64_t off_n = 0;
         uint32_t L_n = 0;
         if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-        hash_frame<G, PF, 32>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
+        hash_frame<G, PF, 32, ALIGNED>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
         f = fn;
         off = off_n;
         L = L_n;
@@ -358,7 +371,7 @@ __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, boo
 {
     constexpr int G = class_lanes(C);
     const int lane = threadIdx.x & 63;
-    hash_frame<G, PF, 16>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
+    hash_frame<G, PF, 16, false>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
 }
 
 // Ragged batches: persistent grid; every wave walks the items (64/G frames of

@@ -126,10 +126,22 @@ void fill_constants(FrameParams &p)
 }
 
 template <int G>
-void launch_uniform_g(bool pf, dim3 grid, hipStream_t s, const FrameParams &p)
+void launch_uniform_g(bool pf, bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
 {
-    if (pf) hipLaunchKernelGGL((k_frames<G, true>), grid, dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((k_frames<G, false>), grid, dim3(kBlock), 0, s, p);
+    if (pf && aligned) hipLaunchKernelGGL((k_frames<G, true, true>), grid, dim3(kBlock), 0, s, p);
+    else if (pf) hipLaunchKernelGGL((k_frames<G, true, false>), grid, dim3(kBlock), 0, s, p);
+    else if (aligned) hipLaunchKernelGGL((k_frames<G, false, true>), grid, dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL((k_frames<G, false, false>), grid, dim3(kBlock), 0, s, p);
+}
+
+// Every unit start is dword-aligned when frames are strided with a 4-multiple
+// stride and (base + L) is 4-aligned for both lengths: a unit starts at
+// base + f*stride + L - 64k. Descriptor batches take the realigning loads.
+bool units_dword_aligned(const FrameParams &p)
+{
+    if (p.off) return false;
+    const uintptr_t b = (uintptr_t)p.base;
+    return p.stride % 4 == 0 && (b + p.flen) % 4 == 0 && (b + p.last_len) % 4 == 0;
 }
 
 val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
@@ -140,15 +152,15 @@ val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
-    const bool pf = prefetch_on();
+    const bool pf = prefetch_on(), aligned = units_dword_aligned(p);
     switch (G) {
-    case 1: launch_uniform_g<1>(pf, grid, s, p); break;
-    case 2: launch_uniform_g<2>(pf, grid, s, p); break;
-    case 4: launch_uniform_g<4>(pf, grid, s, p); break;
-    case 8: launch_uniform_g<8>(pf, grid, s, p); break;
-    case 16: launch_uniform_g<16>(pf, grid, s, p); break;
-    case 32: launch_uniform_g<32>(pf, grid, s, p); break;
-    case 64: launch_uniform_g<64>(pf, grid, s, p); break;
+    case 1: launch_uniform_g<1>(pf, aligned, grid, s, p); break;
+    case 2: launch_uniform_g<2>(pf, aligned, grid, s, p); break;
+    case 4: launch_uniform_g<4>(pf, aligned, grid, s, p); break;
+    case 8: launch_uniform_g<8>(pf, aligned, grid, s, p); break;
+    case 16: launch_uniform_g<16>(pf, aligned, grid, s, p); break;
+    case 32: launch_uniform_g<32>(pf, aligned, grid, s, p); break;
+    case 64: launch_uniform_g<64>(pf, aligned, grid, s, p); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
