@@ -23,8 +23,8 @@ def load(path):
 def workload(name, dev):
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    if name == "cfg3":
-        n, L = 1 << 20, 16384 - 4
+    if name in ("cfg3", "cfg3b"):  # cfg3b: the bench layout (flen 16400, stride 16404)
+        n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
     rng = np.random.default_rng(1)

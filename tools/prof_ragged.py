@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Profiling target for the ragged path. mode: strided57 | ragged57 | mix3 | mix3aligned"""
+"""Profiling target for the ragged path.
+usage: prof_ragged.py MODE [LIB]   MODE: strided57 | ragged57 | mix3 | mix3aligned
+LIB: optional other build of libval_crc_hip.so (A/B under the profiler)."""
 import os
 import sys
 
@@ -11,6 +13,10 @@ import val_protocol_amd.crc as vc  # noqa: E402
 
 mode = sys.argv[1]
 dev = torch.device("cuda:0")
+if len(sys.argv) > 2:
+    from tools.ab_libs import load  # noqa: E402
+
+    vc._lib = load(sys.argv[2])
 vc.init(0)
 rng = np.random.default_rng(1)
 if mode in ("strided57", "ragged57"):
