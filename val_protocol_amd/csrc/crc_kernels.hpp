@@ -138,6 +138,22 @@ __device__ __forceinline__ void frame_desc(const FrameParams &p, uint64_t f, uin
     }
 }
 
+// Register after feeding words first..15 of w into a zero register
+// (first is wave-uniform: a scalar jump into the unrolled steps).
+__device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)[kWords], const SliceBases &sb)
+{
+    uint32_t acc = 0;
+    switch (first) {
+#define VCRC_STEP(i) \
+    case i: acc = s4_step(acc, w[i], sb); [[fallthrough]];
+        VCRC_STEP(0) VCRC_STEP(1) VCRC_STEP(2) VCRC_STEP(3) VCRC_STEP(4) VCRC_STEP(5) VCRC_STEP(6) VCRC_STEP(7)
+        VCRC_STEP(8) VCRC_STEP(9) VCRC_STEP(10) VCRC_STEP(11) VCRC_STEP(12) VCRC_STEP(13) VCRC_STEP(14) VCRC_STEP(15)
+#undef VCRC_STEP
+    default: break;
+    }
+    return acc;
+}
+
 // Hash frame f (at base + off, L bytes) with the G lanes of this lane's group
 // (g = 0..G-1). All 64 lanes of the wave must call this together (the merge
 // tree shuffles); inactive lanes pass L = 0.
@@ -156,14 +172,21 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     uint32_t nxt[kWords];
     if (PF && R > 1) load_full<ALIGNED>(nxt, up, b);
     uint32_t acc = 0;
+    // Round 0's leading zero words (unit 0's front padding, lanes without a
+    // unit) leave the zero register unchanged: the wave starts at the first
+    // word any lane needs (e.g. 16,400-B frames: 257 units, round 0 = one
+    // unit holding 16 real bytes -> 4 steps instead of 16).
+    int first = (R == 0 || u0 < 0) ? kWords : (u0 == 0 ? (int)(pad >> 2) : 0);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
+    first = __builtin_amdgcn_readfirstlane(first);
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
         uint32_t w[kWords];
         bool tiny;
         load_unit0<ALIGNED>(w, u0, fp, L, pad, seed, tiny);
-#pragma unroll
-        for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
+        acc = s4_words_from(first, w, sb);
         if (tiny) {  // L < 4: state of the few bytes straight from the seed
             acc = seed;
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
