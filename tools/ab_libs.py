@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B two builds of libval_crc_hip.so in one process on the same inputs:
 interleaved timing of val_crc32_frames_dev (tooling only, not the product).
-usage: ab_libs.py LIB_A LIB_B [cfg3|cfg5|u57]..."""
+usage: ab_libs.py LIB_A LIB_B [cfg3|cfg3b|cfg5|cfg5log|u57]..."""
 import ctypes
 import os
 import sys
@@ -27,11 +27,18 @@ def workload(name, dev):
         n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    if name == "cfg5log":  # bench.py cfg5: log-uniform payloads with DATA headers (rank 0 sample)
+        import bench
+
+        buf, off, length = bench.make_ragged_frames(torch, dev, bench.CONFIGS["cfg5"][0], seed=1234)
+        return dict(buf=buf, off=off, length=length, len_hint=0), int(length.long().sum().item())
     rng = np.random.default_rng(1)
     if name == "cfg5":
         lens = rng.integers(520, 65533, 262144)
     elif name == "u57":
         lens = np.full(56508, 57000)
+    elif name == "u600":
+        lens = np.full(5333154, 600)
     else:
         raise SystemExit(name)
     wire = lens + 4

@@ -1,5 +1,7 @@
-# Round-end measurement: tests, smoke, bench (+host-inclusive), rocprofv3 kernel
-# trace of the bench command, and separate PMC passes for HBM traffic.
+# Round-end measurement: tests, smoke, bench lines (cfg3 headline, verify,
+# cfg4, cfg2, cfg5 ragged), host-inclusive, rocprofv3 kernel trace of the bench
+# command, and separate PMC passes (HBM traffic for cfg3 and cfg5, SQ counters).
+# Then: python tools/round_summary.py gpurun_out/round 1  (on the CPU side).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/round
@@ -10,11 +12,15 @@ timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && \
 timeout -k 10 600 python bench.py --verify --no-cpu-baseline > $O/bench_verify.json 2> $O/bench_verify.err && \
 timeout -k 10 600 python bench.py --config cfg4 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err && \
 timeout -k 10 600 python bench.py --config cfg2 --no-cpu-baseline --steps 200 > $O/bench_cfg2.json 2> $O/bench_cfg2.err && \
+timeout -k 10 600 python bench.py --config cfg5 --no-cpu-baseline > $O/bench_cfg5.json 2> $O/bench_cfg5.err && \
 timeout -k 10 600 python tools/host_inclusive.py > $O/host_inclusive.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 $R/bench.py --steps 10 --no-cpu-baseline > $O/trace.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace5 -o bench -- python3 $R/bench.py --config cfg5 --steps 10 --no-cpu-baseline > $O/trace5.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_v -o p -- python3 $R/tools/prof_target.py cfg3 3 verify > $O/pmc_fetch_v.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch5 -o p -- python3 $R/tools/prof_target.py cfg5 3 > $O/pmc_fetch5.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write5 -o p -- python3 $R/tools/prof_target.py cfg5 3 > $O/pmc_write5.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_sq.log 2>&1
 echo "round profile rc=$?"

@@ -16,18 +16,29 @@ verify = len(sys.argv) > 3 and sys.argv[3] == "verify"
 dev = torch.device("cuda:0")
 vc.init(0)
 n, payload, explicit, header = bench.CONFIGS[cfg]
-buf, flen, stride = bench.make_frames(torch, dev, n, payload, explicit, 0, 11)
-flat = buf.view(-1)
 crc = torch.empty(n, dtype=torch.int32, device=dev)
 hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
+if cfg == "cfg5":  # ragged descriptor batch, binned on the device (len_hint 0)
+    flat, d_off, d_len = bench.make_ragged_frames(torch, dev, n, seed=1234)  # = bench.py rank 0
+    kw = dict(off=d_off, length=d_len, len_hint=0)
+    alg = int(d_len.long().sum().item())
+else:
+    buf, flen, stride = bench.make_frames(torch, dev, n, payload, explicit, 0, 11)
+    flat = buf.view(-1)
+    kw = dict(stride=stride, flen=flen, n=n)
+    alg = n * flen
 if verify:
-    vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc)
-    buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
+    vc.frames(flat, out_crc=crc, **kw)
+    if cfg == "cfg5":
+        tidx = ((d_off + d_len.long())[:, None] + torch.arange(4, device=dev)[None, :]).reshape(-1)
+        flat[tidx] = crc.view(torch.uint8)
+    else:
+        buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
 torch.cuda.synchronize()
 for _ in range(reps):
     if verify:
-        vc.verify_frames(flat, stride=stride, flen=flen, n=n, out_hdr=hdr)
+        vc.verify_frames(flat, out_hdr=hdr, **kw)
     else:
-        vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
+        vc.frames(flat, out_crc=crc, out_hdr=hdr, **kw)
 torch.cuda.synchronize()
-print(f"{cfg}: {reps} launches of {n} frames x {flen} B CRC input, lanes/frame {vc.lanes_per_frame(flen)}")
+print(f"{cfg}: {reps} launches of {n} frames, algorithmic_bytes_per_launch {alg}")

@@ -266,19 +266,26 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 }
 
 // ---- ragged path ------------------------------------------------------------
-// Frames are counting-sorted by length bucket (512 B wide, longest first) so
-// the 64/G frames a wave hashes together have nearly equal lengths, and the
-// sorted order is cut into geometry classes (contiguous bucket ranges).
-constexpr int kBucketBytes = 512;
-constexpr int kBuckets = 129;  // [0,512), ..., [65024,65536), [65536, inf)
+// Frames are counting-sorted by length bucket, longest first, so the 64/G
+// frames a wave hashes together need the same number of rounds, and the
+// sorted order is cut into geometry classes (contiguous bucket ranges). A
+// bucket is one round of its class (G * 64 bytes): within a bucket every
+// frame has R = ceil(L / (64 G)) rounds, so no lane idles behind a longer
+// neighbour (round 0 is partial, and nearly free: s4_words_from).
+//   class 0 (G=2,  128 B rounds): L in [0, 1024)       buckets 0..7
+//   class 1 (G=4,  256 B rounds): L in [1024, 8192)    buckets 8..36
+//   class 2 (G=8,  512 B rounds): L in [8192, 49152)   buckets 37..117
+//   class 3 (G=16, 1 KiB rounds): L in [49152, 65536]  buckets 118..134, longer 135
+constexpr int kBuckets = 136;
 __host__ __device__ inline int length_bucket(uint32_t L)
 {
-    const uint32_t b = L / kBucketBytes;
-    return b < (uint32_t)(kBuckets - 1) ? (int)b : kBuckets - 1;
+    if (L < 1024u) return L <= 128u ? 0 : (int)((L - 1u) / 128u);
+    if (L < 8192u) return 8 + (int)((L - 1u) / 256u) - 3;
+    if (L < 49152u) return 37 + (int)((L - 1u) / 512u) - 15;
+    const uint32_t r = (L - 1u) / 1024u;  // 47.. for L >= 49152
+    return r < 64u ? 118 + (int)r - 47 : kBuckets - 1;
 }
-// Sorted position of a bucket: longest bucket first.
-__host__ __device__ inline int bucket_rank(int b) { return kBuckets - 1 - b; }
-__host__ __device__ inline int bucket_class(int b) { return length_class((uint32_t)b * kBucketBytes); }
+__host__ __device__ inline int bucket_class(int b) { return b < 8 ? 0 : b < 37 ? 1 : b < 118 ? 2 : 3; }
 
 // Pass 1: per-workgroup bucket counts; each workgroup reserves its slice of
 // every non-empty bucket with one atomic (offsets within the bucket) and adds
@@ -345,8 +352,12 @@ __global__ __launch_bounds__(256) void k_bin_plan(const uint32_t *gcount, const 
     ctab[12] = item;  // total items
 }
 
-// Pass 3: scatter frame indices into sorted order (order within a bucket is
-// unspecified; every output is written at its frame's own index).
+// Pass 3: scatter frame indices into sorted order. Wave-aggregated: the
+// lanes of a wave that share a bucket take consecutive slots in lane order
+// (one LDS atomic per bucket per wave step), so runs of up to 64 consecutive
+// frames stay adjacent in the sorted order and the frames a wave hashes
+// together are mostly neighbours in memory. Order across waves is
+// unspecified; every output is written at its frame's own index.
 __global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32_t n, uint32_t chunk,
                                                      const uint32_t *bstart, const uint32_t *blockoff, uint32_t *order)
 {
@@ -354,8 +365,25 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32
     for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
         cur[b] = bstart[b] + blockoff[(size_t)blockIdx.x * kBuckets + b];
     __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) order[atomicAdd(&cur[length_bucket(len[i])], 1u)] = (uint32_t)i;
+    for (uint64_t base = lo; base < hi; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool v = i < hi;
+        const int b = v ? length_bucket(len[i]) : -1;
+        uint64_t pending = __ballot(v);
+        while (pending) {  // wave-uniform: one bucket per pass
+            const int leader = __ffsll((long long)pending) - 1;
+            const int bl = __shfl(b, leader);
+            const uint64_t grp = __ballot(v && b == bl);
+            uint32_t pos = 0;
+            if (lane == leader) pos = atomicAdd(&cur[bl], (uint32_t)__popcll(grp));
+            pos = __shfl(pos, leader);
+            if (v && b == bl) order[pos + (uint32_t)__popcll(grp & below)] = (uint32_t)i;
+            pending &= ~grp;
+        }
+    }
 }
 
 // Item `it` of the ragged plan: its class and sorted-order range.
