@@ -286,78 +286,98 @@ __host__ __device__ inline int length_bucket(uint32_t L)
     return r < 64u ? 118 + (int)r - 47 : kBuckets - 1;
 }
 __host__ __device__ inline int bucket_class(int b) { return b < 8 ? 0 : b < 37 ? 1 : b < 118 ? 2 : 3; }
+constexpr int kClassFirstBucket[kClasses + 1] = {0, 8, 37, 118, kBuckets};
 
-// Pass 1: per-workgroup bucket counts; each workgroup reserves its slice of
-// every non-empty bucket with one atomic (offsets within the bucket) and adds
-// the bucket's bytes. gcount/gbytes must be zero on entry.
-__global__ __launch_bounds__(256) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk, uint32_t *gcount,
-                                                   unsigned long long *gbytes, uint32_t *blockoff)
+// A wave's lanes that all hold the same bucket (uniform batches) reserve
+// their slots with one LDS atomic; mixed waves use one atomic per lane.
+// Returns this lane's slot offset from cnt[b] (v: the lane holds an element).
+__device__ __forceinline__ uint32_t bucket_slot(uint32_t *cnt, int b, bool v)
 {
-    __shared__ uint32_t cnt[kBuckets];
-    __shared__ unsigned long long bytes[kBuckets];
-    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) {
-        cnt[b] = 0;
-        bytes[b] = 0;
+    const int lane = threadIdx.x & 63;
+    const uint64_t act = __ballot(v);
+    if (act == 0) return 0;
+    const int leader = __ffsll((long long)act) - 1;
+    const int b0 = __shfl(b, leader);
+    if (__ballot(v && b != b0) == 0) {
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cnt[b0], (uint32_t)__popcll(act));
+        base = __shfl(base, leader);
+        return base + (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
     }
-    __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const uint32_t L = len[i];
-        const int b = length_bucket(L);
-        atomicAdd(&cnt[b], 1u);
-        atomicAdd(&bytes[b], (unsigned long long)L);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) {
-        uint32_t off = 0;
-        if (cnt[b]) {
-            off = atomicAdd(&gcount[b], cnt[b]);
-            atomicAdd(&gbytes[b], bytes[b]);
-        }
-        blockoff[(size_t)blockIdx.x * kBuckets + b] = off;
-    }
+    return v ? atomicAdd(&cnt[b], 1u) : 0u;
 }
 
-// Pass 2 (one workgroup): bucket starts in sorted order (longest first) and
-// the class table: class c occupies sorted positions [cstart, cstart+ccount)
-// and is cut into items of 64/G_c frames (one wave step each); items are
-// numbered longest class first: class c owns items [istart[c], istart[c+1]).
-// ctab = {cstart[4], ccount[4], istart[5]}.
-__global__ __launch_bounds__(256) void k_bin_plan(const uint32_t *gcount, const unsigned long long *gbytes,
-                                                  uint32_t *bstart, uint32_t *ctab)
+// Pass 1: per-workgroup bucket counts; each workgroup reserves its slice of
+// every non-empty bucket with one atomic (offsets within the bucket).
+// gcount must be zero on entry.
+__global__ __launch_bounds__(256) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk, uint32_t *gcount,
+                                                   uint32_t *blockoff)
 {
     __shared__ uint32_t cnt[kBuckets];
-    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cnt[b] = gcount[b];
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    (void)gbytes;
-    uint32_t ccount[kClasses] = {}, cstart[kClasses];
-    for (int c = 0; c < kClasses; c++) cstart[c] = 0xFFFFFFFFu;
-    uint32_t pos = 0;
-    for (int r = 0; r < kBuckets; r++) {  // longest bucket first
-        const int b = kBuckets - 1 - r, c = bucket_class(b);
-        bstart[b] = pos;
-        if (cnt[b] && pos < cstart[c]) cstart[c] = pos;
-        ccount[c] += cnt[b];
-        pos += cnt[b];
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
+    for (uint64_t base = lo; base < hi; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool v = i < hi;
+        (void)bucket_slot(cnt, v ? length_bucket(len[i]) : 0, v);
     }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
+        blockoff[(size_t)blockIdx.x * kBuckets + b] = cnt[b] ? atomicAdd(&gcount[b], cnt[b]) : 0u;
+}
+
+// Pass 2 (one wave): bucket starts in sorted order (longest bucket first) by a
+// wave prefix scan, and the class table: class c occupies sorted positions
+// [cstart, cstart+ccount) and is cut into items of 64/G_c frames (one wave
+// step each); items are numbered longest class first: class c owns items
+// [istart[c], istart[c+1]). ctab = {cstart[4], ccount[4], istart[5]}.
+__global__ __launch_bounds__(64) void k_bin_plan(const uint32_t *gcount, uint32_t *bstart, uint32_t *ctab)
+{
+    constexpr int kPer = (kBuckets + 63) / 64;
+    __shared__ uint32_t rank_pos[kBuckets + 1];  // sorted start of rank r (bucket kBuckets-1-r)
+    const int l = threadIdx.x;
+    uint32_t c[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int r = l * kPer + k;
+        c[k] = r < kBuckets ? gcount[kBuckets - 1 - r] : 0u;
+        sum += c[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o);
+        if (l >= o) inc += t;
+    }
+    uint32_t pos = inc - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int r = l * kPer + k;
+        if (r < kBuckets) {
+            bstart[kBuckets - 1 - r] = pos;
+            rank_pos[r] = pos;
+        }
+        pos += c[k];
+    }
+    if (l == 63) rank_pos[kBuckets] = inc;
+    __syncthreads();
+    if (l != 0) return;
     uint32_t item = 0;
-    for (int c = kClasses - 1; c >= 0; c--) {
-        const uint32_t per = 64u / (uint32_t)class_lanes(c);
-        ctab[8 + c] = item;
-        item += (ccount[c] + per - 1) / per;
-        ctab[c] = ccount[c] ? cstart[c] : 0u;
-        ctab[4 + c] = ccount[c];
+    for (int cc = kClasses - 1; cc >= 0; cc--) {  // class cc = ranks [kBuckets - first[cc+1], kBuckets - first[cc])
+        const uint32_t cstart = rank_pos[kBuckets - kClassFirstBucket[cc + 1]];
+        const uint32_t ccount = rank_pos[kBuckets - kClassFirstBucket[cc]] - cstart;
+        const uint32_t per = 64u / (uint32_t)class_lanes(cc);
+        ctab[8 + cc] = item;
+        item += (ccount + per - 1) / per;
+        ctab[cc] = ccount ? cstart : 0u;
+        ctab[4 + cc] = ccount;
     }
     ctab[12] = item;  // total items
 }
 
-// Pass 3: scatter frame indices into sorted order. Wave-aggregated: the
-// lanes of a wave that share a bucket take consecutive slots in lane order
-// (one LDS atomic per bucket per wave step), so runs of up to 64 consecutive
-// frames stay adjacent in the sorted order and the frames a wave hashes
-// together are mostly neighbours in memory. Order across waves is
-// unspecified; every output is written at its frame's own index.
+// Pass 3: scatter frame indices into sorted order (order within a bucket is
+// unspecified; every output is written at its frame's own index).
 __global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32_t n, uint32_t chunk,
                                                      const uint32_t *bstart, const uint32_t *blockoff, uint32_t *order)
 {
@@ -365,24 +385,12 @@ __global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32
     for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
         cur[b] = bstart[b] + blockoff[(size_t)blockIdx.x * kBuckets + b];
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1ull;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
     for (uint64_t base = lo; base < hi; base += blockDim.x) {
         const uint64_t i = base + threadIdx.x;
         const bool v = i < hi;
-        const int b = v ? length_bucket(len[i]) : -1;
-        uint64_t pending = __ballot(v);
-        while (pending) {  // wave-uniform: one bucket per pass
-            const int leader = __ffsll((long long)pending) - 1;
-            const int bl = __shfl(b, leader);
-            const uint64_t grp = __ballot(v && b == bl);
-            uint32_t pos = 0;
-            if (lane == leader) pos = atomicAdd(&cur[bl], (uint32_t)__popcll(grp));
-            pos = __shfl(pos, leader);
-            if (v && b == bl) order[pos + (uint32_t)__popcll(grp & below)] = (uint32_t)i;
-            pending &= ~grp;
-        }
+        const uint32_t slot = bucket_slot(cur, v ? length_bucket(len[i]) : 0, v);
+        if (v) order[slot] = (uint32_t)i;
     }
 }
 
