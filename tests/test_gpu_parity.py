@@ -322,3 +322,35 @@ def test_empty_batches(vc, dev):
     out2 = vc.frames(d, stride=4, flen=4, n=0)
     torch.cuda.synchronize()
     assert out.numel() == 0 and out2.numel() == 0
+
+
+# Batches whose frame groups leave a partial last wave-round (256 CUs x 16
+# waves on MI355X): the library re-cuts those frames with more lanes per frame
+# in a second launch. Strided and descriptor mode, header_crc, verify with a
+# corrupted frame inside the tail, and a byte-misaligned base.
+@pytest.mark.parametrize("L,extra", [(60000, 37), (1000, 1000), (16400, 4097), (4200, 1)])
+def test_wave_round_tail(vc, dev, L, extra):
+    per = 64 // vc.lanes_per_frame(L)
+    n = 256 * 16 * per + extra
+    stride = L + 4
+    g = torch.Generator(device=dev).manual_seed(L + extra)
+    raw = torch.randint(0, 256, (n * stride + 3,), dtype=torch.uint8, device=dev, generator=g)
+    buf = raw[3:]
+    host = buf.cpu().numpy()
+    want, want_h = _oracle.frames_strided(host, stride, L, n, header=True, nthreads=16)
+    hdr = torch.empty(n, dtype=torch.int32, device=dev)
+    crc = vc.frames(buf, stride=stride, flen=L, n=n, out_hdr=hdr)
+    offs = torch.arange(n, dtype=torch.int64, device=dev) * stride
+    lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+    crc_d = vc.frames(buf, off=offs, length=lens, len_hint=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(crc), want)
+    assert np.array_equal(_u32(hdr), want_h)
+    assert np.array_equal(_u32(crc_d), want)
+    buf.view(n, stride)[:, L:L + 4] = crc.view(torch.uint8).view(n, 4)
+    bad = n - 2
+    buf[bad * stride + L // 2] ^= 0x10
+    ok, nbad = vc.verify_frames(buf, stride=stride, flen=L, n=n)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy()
+    assert int(nbad.item()) == 1 and int(okh.argmin()) == bad and int(okh.sum()) == n - 1

@@ -37,15 +37,21 @@ def workload(name, dev):
         lens = rng.integers(520, 65533, 262144)
     elif name == "u57":
         lens = np.full(56508, 57000)
-    elif name == "u600":
-        lens = np.full(5333154, 600)
+    elif name in ("c2", "c2a"):  # class-2 log-uniform mix; c2a: lengths = 12 mod 16 (16-B aligned frame starts)
+        lens = np.exp(rng.uniform(np.log(8192), np.log(49151), 150000)).astype(np.int64)
+        if name == "c2a":
+            lens = (lens // 16) * 16 + 12
+    elif name.startswith("u") and name.rstrip("d")[1:].isdigit():  # uNNNN: uniform length NNNN, ragged path;
+        L = int(name.rstrip("d")[1:])                              # uNNNNd: same, descriptor-uniform (len_hint)
+        lens = np.full(max(1, (3 << 30) // (L + 4)), L)
     else:
         raise SystemExit(name)
     wire = lens + 4
     off = np.concatenate([[0], np.cumsum(wire)[:-1]])
     buf = torch.randint(0, 256, (int(wire.sum()),), dtype=torch.uint8, device=dev, generator=g)
     return dict(buf=buf, off=torch.from_numpy(off.astype(np.int64)).to(dev),
-                length=torch.from_numpy(lens.astype(np.int32)).to(dev), len_hint=0), int(lens.sum())
+                length=torch.from_numpy(lens.astype(np.int32)).to(dev),
+                len_hint=int(lens[0]) if name.endswith("d") else 0), int(lens.sum())
 
 
 def main():
@@ -62,7 +68,7 @@ def main():
                 vc._lib = l
                 out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
                 if "off" in w:
-                    fn = lambda: vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=0)
+                    fn = lambda: vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=w["len_hint"])
                 else:
                     fn = lambda: vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
                 med, _ = time_it(fn, reps=10)

@@ -18,7 +18,7 @@ w, _ = workload(sys.argv[1], dev)
 out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
 for _ in range(3):
     if "off" in w:
-        vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=0)
+        vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=w["len_hint"])
     else:
         vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
 torch.cuda.synchronize()

@@ -144,7 +144,7 @@ bool units_dword_aligned(const FrameParams &p)
     return p.stride % 4 == 0 && (b + p.flen) % 4 == 0 && (b + p.last_len) % 4 == 0;
 }
 
-val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
+val_status_t launch_uniform_one(FrameParams &p, uint32_t G, hipStream_t s)
 {
     fill_constants(p);
     p.xgap[0] = gf2_x8n((uint64_t)(G - 1) * kUnit);
@@ -165,6 +165,39 @@ val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
     return VAL_OK;
+}
+
+// Persistent waves take whole frame groups, so a launch lasts
+// ceil(groups / waves) group-times: 131,113 frames of 64 KiB at G = 16 are
+// 8.002 wave-rounds, the last one 99.8% idle. The frames of a partial last
+// round are re-cut with more lanes per frame (up to 64) into a second launch
+// on the same stream, so the tail costs about G / G_tail of a group-time.
+val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
+{
+    const uint64_t per = 64 / G, groups = (p.n + per - 1) / per;
+    const uint64_t waves = (uint64_t)g_ctx.cus * kWavesPerBlock;
+    const uint64_t full = groups / waves;
+    uint32_t Gt = G;
+    const uint64_t n_main = full * waves * per, n_tail = p.n - std::min<uint64_t>(p.n, n_main);
+    if (full > 0 && n_tail > 0)
+        while (Gt < 64 && (n_tail + 64 / (2 * Gt) - 1) / (64 / (2 * Gt)) <= waves) Gt *= 2;
+    if (Gt == G) return launch_uniform_one(p, G, s);
+    FrameParams m = p, t = p;
+    m.n = (uint32_t)n_main;
+    t.n = (uint32_t)n_tail;
+    if (p.off) {
+        t.off = p.off + n_main;
+        t.len = p.len + n_main;
+    } else {
+        m.last_len = p.flen;
+        t.base = p.base + n_main * p.stride;
+    }
+    t.seed0 = p.seed_rest;  // frame 0 is in the main part
+    if (p.out_crc) t.out_crc = p.out_crc + n_main;
+    if (p.out_hdr) t.out_hdr = p.out_hdr + n_main;
+    if (p.out_ok) t.out_ok = p.out_ok + n_main;
+    val_status_t st = launch_uniform_one(m, G, s);
+    return st == VAL_OK ? launch_uniform_one(t, Gt, s) : st;
 }
 
 // Ragged descriptor batch: counting-sort by length on the device, then one
