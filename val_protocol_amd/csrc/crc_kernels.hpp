@@ -52,6 +52,7 @@ struct FrameParams {
     uint32_t verify;
     const uint32_t *order;   // grouped mode: class-sorted frame indices
     const uint32_t *plan;    // ragged mode: class table {cstart[4], ccount[4], istart[5]}
+    uint32_t *heads;         // ragged mode: 8 work-queue heads, 64 B apart, zero on entry
     uint32_t xtab[4];        // x^(8(k+1)): slice table T_k
     uint32_t xgap[kClasses]; // x^(8 (G-1) 64) per geometry (index 0 in uniform mode)
     uint32_t tree[kMaxTree][32];  // columns of "advance 64 * 2^j bytes"
@@ -433,10 +434,18 @@ __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, boo
     hash_frame<G, PF, 16, false>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
 }
 
-// Ragged batches: persistent grid; every wave walks the items (64/G frames of
-// one class, longest first) cyclically, fetching the next item's descriptors
-// while it hashes the current one. All four classes' gap maps stay in LDS, so
-// waves never synchronise after the prologue.
+// Ragged batches: persistent grid; waves pull items (64/G frames of one
+// class, longest first) from a work queue, so the launch ends about one item
+// after the bytes run out (longest-processing-time-first: a static cyclic deal
+// gave wave 0 the longest item of every round). The queue is split into P <= 8
+// interleaved partitions (item = part + P * k), one head word each, keyed by
+// blockIdx % P -- on MI355X that is the workgroup's XCD, so a head is only
+// pulled by the 512 waves of one XCD (one word saturates near 88 dequeues/us).
+// Every partition has at least one workgroup (P <= gridDim.x), so every item
+// is hashed exactly once whatever the placement. A wave's first two items are
+// static; item i + 2 is dequeued while item i hashes and item i + 1's
+// descriptors load, so neither latency is exposed. All four classes' gap maps
+// stay in LDS: waves never synchronise after the prologue.
 template <bool PF>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
@@ -450,22 +459,29 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     const uint32_t items = ctab[12];
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
-    const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * kBlock) >> 6;
-    uint32_t it = wave;
+    const uint32_t P = min(8u, gridDim.x);
+    const uint32_t part = blockIdx.x % P;
+    const uint32_t nwp = ((gridDim.x - part + P - 1) / P) * kWavesPerBlock;  // waves of this partition
+    uint32_t *head = p.heads + part * 16u;  // 64 B apart
+    const uint32_t k0 = (blockIdx.x / P) * kWavesPerBlock + (threadIdx.x >> 6);
+    uint32_t it = part + P * k0;
     if (it >= items) return;
+    uint32_t it_n = part + P * (k0 + nwp);  // second item: static
     Item cur = ragged_item(ctab, it);
     uint64_t f, off;
     uint32_t L;
     bool active;
     item_frame(p, cur, lane, f, active, off, L);
-    for (; it < items; it += nwaves) {
+    while (true) {
+        // dequeue item i + 2 (its index is only needed next iteration)
+        uint32_t k_nn = 0;
+        if (it_n < items && lane == 0) k_nn = atomicAdd(head, 1u);
         Item nxt{0, 0, 0};
         uint64_t f_n = 0, off_n = 0;
         uint32_t L_n = 0;
         bool active_n = false;
-        if (it + nwaves < items) {
-            nxt = ragged_item(ctab, it + nwaves);
+        if (it_n < items) {
+            nxt = ragged_item(ctab, it_n);
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
         switch (cur.c) {
@@ -474,6 +490,9 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
         case 1: hash_class<1, PF>(p, f, active, off, L, sb); break;
         default: hash_class<0, PF>(p, f, active, off, L, sb); break;
         }
+        if (it_n >= items) break;
+        it = it_n;
+        it_n = part + P * (__builtin_amdgcn_readfirstlane(k_nn) + 2u * nwp);
         cur = nxt;
         f = f_n;
         off = off_n;

@@ -207,18 +207,19 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
     const uint32_t n = p.n;
     const uint32_t nbin = std::max(1u, std::min(1024u, (n + 2047u) / 2048u));
     const uint32_t chunk = (n + nbin - 1) / nbin;
-    // scratch: gcount[kBuckets] u32 (zeroed) | bstart[kBuckets] u32 | ctab[16] u32 |
-    //          blockoff[nbin][kBuckets] u32 | order[n] u32
-    const size_t sz_gcount = (size_t)kBuckets * 4u;
-    const size_t total = 2 * sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
+    // scratch: heads[8][16] u32 + gcount[kBuckets] u32 (both zeroed) | bstart[kBuckets] u32 |
+    //          ctab[16] u32 | blockoff[nbin][kBuckets] u32 | order[n] u32
+    const size_t sz_heads = 8u * 64u, sz_gcount = (size_t)kBuckets * 4u;
+    const size_t total = sz_heads + 2 * sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     uint8_t *scratch = nullptr;
     VCRC_HIP(hipMallocAsync((void **)&scratch, total, s), "hipMallocAsync(bin scratch)");
-    uint32_t *gcount = reinterpret_cast<uint32_t *>(scratch);
+    uint32_t *heads = reinterpret_cast<uint32_t *>(scratch);
+    uint32_t *gcount = heads + sz_heads / 4u;
     uint32_t *bstart = gcount + kBuckets;
     uint32_t *ctab = bstart + kBuckets;
     uint32_t *blockoff = ctab + 16;
     uint32_t *order = blockoff + (size_t)nbin * kBuckets;
-    hipError_t e = hipMemsetAsync(scratch, 0, sz_gcount, s);
+    hipError_t e = hipMemsetAsync(scratch, 0, sz_heads + sz_gcount, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, gcount, blockoff);
         hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, gcount, bstart, ctab);
@@ -227,6 +228,7 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
         for (int c = 0; c < kClasses; c++) p.xgap[c] = gf2_x8n((uint64_t)(class_lanes(c) - 1) * kUnit);
         p.order = order;
         p.plan = ctab;
+        p.heads = heads;
         // persistent: enough waves for the items, at most one workgroup per CU
         const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
         const unsigned blocks = (unsigned)std::max<uint64_t>(
