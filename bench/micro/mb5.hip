@@ -1,0 +1,63 @@
+// Microbenchmark 5: fixed cost of one frames launch (run under rocprofv3
+// --kernel-trace; durations come from the trace). Kernels:
+//   k_empty          256 x 1024 threads, 160 KiB LDS, no work
+//   k_prologue       the frames kernel's LDS table build only
+//   k_frames<64,1>   the product kernel on 1..N tiny frames (one wave each)
+// Not product code.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+
+#include "crc_kernels.hpp"
+
+#define CHECK(x) do{hipError_t e_=(x); if(e_!=hipSuccess){printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);}}while(0)
+
+__global__ __launch_bounds__(1024) void k_empty(uint32_t* out){ vcrc::s_lds[threadIdx.x] = threadIdx.x; __syncthreads(); if (vcrc::s_lds[(threadIdx.x + 1) & 1023] == 7777u) out[0] = 1; }
+
+__global__ __launch_bounds__(1024) void k_prologue(const vcrc::FrameParams p, uint32_t* out){
+  const int gi[1] = {6};
+  vcrc::build_lds_tables<1, 32>(p.consts, gi, vcrc::kLdsGap, 6);
+  __syncthreads();
+  if (vcrc::s_lds[threadIdx.x * 37] == 7777u) out[0] = 1; }
+
+// prologue pieces: MODE 1 = global load only, 2 = LDS writes of a constant only, 3 = one b128 write per thread
+template <int MODE> __global__ __launch_bounds__(1024) void k_piece(const vcrc::FrameParams p, uint32_t* out){
+  uint32_t v = threadIdx.x * 0x9E3779B1u;
+  if (MODE == 1) v = p.consts[threadIdx.x];
+  if (MODE == 2 || MODE == 3) {
+    uint4 *row = reinterpret_cast<uint4 *>(vcrc::s_lds + (threadIdx.x * 32u) % (128u * 256u));
+    const uint4 vv = make_uint4(v, v, v, v);
+    if (MODE == 2) {
+#pragma unroll
+      for (int r = 0; r < 8; r++) row[r] = vv;
+    } else row[0] = vv;
+  }
+  __syncthreads();
+  if (vcrc::s_lds[threadIdx.x * 37] == 7777u || v == 7777u) out[0] = 1; }
+
+int main(){
+  hipDeviceProp_t pr; CHECK(hipGetDeviceProperties(&pr,0)); int cus=pr.multiProcessorCount;
+  uint8_t* d; CHECK(hipMalloc(&d, 1 << 24)); CHECK(hipMemset(d, 0x5A, 1 << 24));
+  uint32_t* out; CHECK(hipMalloc(&out, 1 << 20));
+  vcrc::FrameParams p; memset(&p, 0, sizeof p);
+  static uint32_t blob[vcrc::kConstWords]; vcrc::fill_const_blob(blob);
+  uint32_t* dc; CHECK(hipMalloc(&dc, sizeof blob)); CHECK(hipMemcpy(dc, blob, sizeof blob, hipMemcpyHostToDevice));
+  p.consts = dc;
+  for (int j = 0; j < vcrc::kMaxTree; j++) gf2_shift_columns((uint64_t)vcrc::kUnit << j, p.tree[j]);
+  p.base = d; p.stride = 1044; p.flen = 1040; p.last_len = 1040; p.seed0 = p.seed_rest = 0xFFFFFFFFu; p.xorout = 0xFFFFFFFFu;
+  p.out_crc = out;
+  for (int r = 0; r < 20; r++) { k_empty<<<cus, 1024>>>(out); CHECK(hipDeviceSynchronize()); }
+  for (int r = 0; r < 20; r++) { k_prologue<<<cus, 1024>>>(p, out); CHECK(hipDeviceSynchronize()); }
+  for (int r = 0; r < 20; r++) { k_prologue<<<16, 1024>>>(p, out); CHECK(hipDeviceSynchronize()); }
+  for (int r = 0; r < 20; r++) { k_piece<1><<<cus, 1024>>>(p, out); CHECK(hipDeviceSynchronize()); }
+  for (int r = 0; r < 20; r++) { k_piece<2><<<cus, 1024>>>(p, out); CHECK(hipDeviceSynchronize()); }
+  for (int r = 0; r < 20; r++) { k_piece<3><<<cus, 1024>>>(p, out); CHECK(hipDeviceSynchronize()); }
+  const uint32_t ns[] = {1, 16, 256, 4096};
+  for (uint32_t n : ns) {
+    p.n = n;
+    const unsigned blocks = (unsigned)((n + 15) / 16 < (uint32_t)cus ? (n + 15) / 16 : cus);
+    for (int r = 0; r < 20; r++) { hipLaunchKernelGGL((vcrc::k_frames<64, 1, true>), dim3(blocks), dim3(1024), 0, 0, p); CHECK(hipDeviceSynchronize()); }
+  }
+  printf("done\n"); return 0; }

@@ -108,8 +108,10 @@ uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);
  * process; 0 restores the automatic choice. Returns VAL_ERR_INVALID_ARG for
  * other values. Results never depend on it; only speed does. */
 val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
-/* Register prefetch of the next round (1 on, 0 off, -1 automatic). */
-val_status_t val_gpu_set_prefetch(int on);
+/* Rounds of each lane's input kept in flight ahead of the one being hashed
+ * (0, 1, 2 or 4; -1 = automatic: 1 for multi-pass batches, deeper when a batch
+ * fits in one pass of the grid). Speed only; results never change. */
+val_status_t val_gpu_set_prefetch(int depth);
 
 #ifdef __cplusplus
 }

@@ -11,8 +11,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 GEOMS = [1, 2, 4, 8, 16, 32, 64]
-# register prefetch off/on variants of the frames kernel
-VARIANTS = [(0,), (1,)]
+# register prefetch depths of the frames kernel (0 = off)
+VARIANTS = [(0,), (1,), (2,), (4,)]
 
 
 @pytest.fixture(scope="module")

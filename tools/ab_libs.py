@@ -23,6 +23,10 @@ def load(path):
 def workload(name, dev):
     g = torch.Generator(device=dev)
     g.manual_seed(1)
+    if name in ("cfg2", "cfg4", "w256"):  # bench layouts: 64 K x 1,040 B; 131,113 x 65,532 B; 256-frame window
+        n, L = {"cfg2": (1 << 16, 1040), "cfg4": (131113, 65532), "w256": (256, 1040)}[name]
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
     if name in ("cfg3", "cfg3b"):  # cfg3b: the bench layout (flen 16400, stride 16404)
         n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

@@ -179,7 +179,7 @@ def lanes_per_frame(typical_len: int) -> int:
 
 
 def set_prefetch(on: int) -> None:
-    """Register prefetch of the next round: 1 on, 0 off, -1 automatic."""
+    """Rounds kept in flight ahead of the hashed one: 0, 1, 2, 4, or -1 automatic."""
     _check(lib().val_gpu_set_prefetch(on), "val_gpu_set_prefetch")
 
 

@@ -94,36 +94,92 @@ __device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *
     return r;
 }
 
-// Prologue, slice tables: T_k from x^(8(k+1)) (xtab), 32 bank replicas.
-__device__ __forceinline__ void build_slice_tables(const uint32_t (&xtab)[4])
+// Device constant blob (u32 words, built once per device at init from
+// gf2_crc32.h and kept in HBM; every launch's prologue copies it into LDS, an
+// L2 hit after the first workgroup):
+//   [kConstSlice, +1024)   T_k[b] at k * 256 + b
+//   [kConstGap,   +7*128)  nibble map "advance (G - 1) * 64 bytes" for G = 2^i,
+//                          entry k * 16 + n = image of n << 4k
+//   [kConstTree,  +6*128)  nibble map "advance 64 * 2^j bytes" (merge level j)
+constexpr uint32_t kConstSlice = 0, kConstGap = 1024, kConstTree = 1024 + 7 * 128;
+constexpr uint32_t kConstWords = kConstTree + kMaxTree * 128;
+constexpr uint32_t kLdsTree = kLdsGap + 16384;  // uniform kernel: 6 x 512 B merge maps after the gap map
+
+// Prologue: the LDS image is written in 16-B chunks, chunk c = r * 1024 + t
+// for thread t, so the 64 lanes of a ds_write_b128 fill 1 KiB contiguously
+// (bank-conflict free; writing each thread's own 128-B table row instead put
+// all lanes 256 B apart and cost 3.4 us per launch). Every thread issues all
+// of its loads from the constant blob before it waits on any of them, so the
+// launch pays one memory latency.
+//   slice tables (128 KiB, 32 bank replicas): chunk c is row c >> 4 (pair =
+//     row >> 8, byte = row & 255), half (c >> 3) & 1 -> T_{3 - (2 pair + half)}[byte];
+//   gap maps: NMAPS maps of 16 x 8 rows (entry k * 16 + n) with REPL replicas,
+//     map m (G = 2^gi[m]) at base + m * 64 * REPL (= its size);
+//   merge maps: thread t < 128 * levels copies one word (one copy each: a
+//     lookup of nibble k reads 16 consecutive words, so lanes never share a bank).
+template <int NMAPS, int REPL>
+__device__ __forceinline__ void build_lds_tables(const uint32_t *consts, const int (&gi)[NMAPS], uint32_t base,
+                                                 int tree_levels)
 {
-    const int t = threadIdx.x;  // thread t: T_k[b], k = t >> 8, b = t & 255
-    const int k = t >> 8, b = t & 255;
-    // constant indices: a per-thread index would spill the kernel arguments to scratch
-    const uint32_t xk = k == 0 ? xtab[0] : k == 1 ? xtab[1] : k == 2 ? xtab[2] : xtab[3];
-    const uint32_t v = gf2_mul(xk, (uint32_t)b);
-    const int slot = 3 - k;
-    uint4 *row = reinterpret_cast<uint4 *>(
-        s_lds + (kLdsS4 + (uint32_t)(slot >> 1) * 65536u + (uint32_t)b * 256u + (uint32_t)(slot & 1) * 128u) / 4);
-    const uint4 vv = make_uint4(v, v, v, v);
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t kMapBytes = 128u * REPL * 4u;              // 128 entries x REPL words
+    constexpr uint32_t kGapChunks = NMAPS * kMapBytes / 16u;      // per workgroup
+    constexpr int kGapPer = (int)((kGapChunks + kBlock - 1) / kBlock);
+    uint32_t v[8], vg[kGapPer];
 #pragma unroll
-    for (int r = 0; r < 8; r++) row[r] = vv;
+    for (int r = 0; r < 8; r++) {
+        const uint32_t c = (uint32_t)r * kBlock + t, row = c >> 4;
+        const uint32_t slot = (row >> 8) * 2u + ((c >> 3) & 1u);
+        v[r] = consts[kConstSlice + (3u - slot) * 256u + (row & 255u)];
+    }
+#pragma unroll
+    for (int r = 0; r < kGapPer; r++) {
+        const uint32_t c = (uint32_t)r * kBlock + t;
+        const uint32_t m = c / (kMapBytes / 16u), entry = (c % (kMapBytes / 16u)) / (REPL / 4u);
+        int g = gi[0];
+#pragma unroll
+        for (int q = 1; q < NMAPS; q++) g = m == (uint32_t)q ? gi[q] : g;
+        vg[r] = c < kGapChunks ? consts[kConstGap + (uint32_t)g * 128u + entry] : 0u;
+    }
+    const bool has_tree = t < (uint32_t)tree_levels * 128u;
+    const uint32_t vt = has_tree ? consts[kConstTree + t] : 0u;
+    uint4 *lds4 = reinterpret_cast<uint4 *>(s_lds);
+#pragma unroll
+    for (int r = 0; r < 8; r++) lds4[(kLdsS4 / 16u) + (uint32_t)r * kBlock + t] = make_uint4(v[r], v[r], v[r], v[r]);
+#pragma unroll
+    for (int r = 0; r < kGapPer; r++) {
+        const uint32_t c = (uint32_t)r * kBlock + t;
+        if (c < kGapChunks) lds4[base / 16u + c] = make_uint4(vg[r], vg[r], vg[r], vg[r]);
+    }
+    if (has_tree) s_lds[kLdsTree / 4 + t] = vt;
 }
 
-// Prologue, one gap map "advance by gap bytes" (xgap = x^(8 gap)) at `base`
-// with REPL replicas: threads 0..127 each build one (table, nibble) row.
-template <int REPL>
-__device__ __forceinline__ void build_gap_table(uint32_t xgap, uint32_t base)
+// Advance register a by 64 * 2^j bytes: 8 nibble lookups in merge map j.
+__device__ __forceinline__ uint32_t tree_step(uint32_t a, int j)
 {
-    const int t = threadIdx.x;
-    if (t < 128) {  // NT_k[n] = gap(n << 4k)
-        const int k = t >> 4, nib = t & 15;
-        const uint32_t v = gf2_mul(xgap, (uint32_t)nib << (4 * k));
-        uint4 *row = reinterpret_cast<uint4 *>(s_lds + (base + (uint32_t)k * (16u * REPL * 4u) + (uint32_t)nib * (REPL * 4u)) / 4);
-        const uint4 vv = make_uint4(v, v, v, v);
+    uint32_t r = 0;
 #pragma unroll
-        for (int r = 0; r < REPL / 4; r++) row[r] = vv;
+    for (int k = 0; k < 8; k++) r ^= lds_read(kLdsTree + (uint32_t)j * 512u + (uint32_t)k * 64u + ((a >> (4 * k)) & 15u) * 4u);
+    return r;
+}
+
+// Host: fill the constant blob (kConstWords u32).
+__host__ inline void fill_const_blob(uint32_t *w)
+{
+    for (int k = 0; k < 4; k++) {
+        const uint32_t xk = gf2_x8n((uint64_t)(k + 1));
+        for (int b = 0; b < 256; b++) w[kConstSlice + k * 256 + b] = gf2_mul(xk, (uint32_t)b);
+    }
+    for (int gi = 0; gi < 7; gi++) {
+        const uint32_t x = gf2_x8n((uint64_t)((1u << gi) - 1u) * kUnit);
+        for (int t = 0; t < 128; t++) w[kConstGap + gi * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
+    }
+    for (int j = 0; j < kMaxTree; j++) {
+        const uint32_t x = gf2_x8n((uint64_t)kUnit << j);
+        for (int t = 0; t < 128; t++) w[kConstTree + j * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
     }
 }
+
+__host__ __device__ constexpr int ilog2(int g) { return g <= 1 ? 0 : 1 + ilog2(g >> 1); }
 
 }  // namespace vcrc

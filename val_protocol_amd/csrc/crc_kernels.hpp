@@ -53,9 +53,8 @@ struct FrameParams {
     const uint32_t *order;   // grouped mode: class-sorted frame indices
     const uint32_t *plan;    // ragged mode: class table {cstart[4], ccount[4], istart[5]}
     uint32_t *heads;         // ragged mode: 8 work-queue heads, 64 B apart, zero on entry
-    uint32_t xtab[4];        // x^(8(k+1)): slice table T_k
-    uint32_t xgap[kClasses]; // x^(8 (G-1) 64) per geometry (index 0 in uniform mode)
-    uint32_t tree[kMaxTree][32];  // columns of "advance 64 * 2^j bytes"
+    const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
+    uint32_t tree[kMaxTree][32];  // columns of "advance 64 * 2^j bytes" (ragged kernel's merge)
 };
 
 // A full 64-B unit starting at byte address up, read with dword-aligned
@@ -158,10 +157,15 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // Hash frame f (at base + off, L bytes) with the G lanes of this lane's group
 // (g = 0..G-1). All 64 lanes of the wave must call this together (the merge
 // tree shuffles); inactive lanes pass L = 0.
-template <int G, bool PF, int REPL, bool ALIGNED>
+// PF = rounds whose 64 B sit in registers ahead of the one being hashed: 1 on
+// long batches (measured best); 2 or 4 when the whole batch is one pass of the
+// grid (small windows: every round's load is issued before the first returns,
+// so a wave pays one HBM latency instead of R - 1).
+template <int G, int PF, int REPL, bool ALIGNED, bool TREE_LDS>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            uint32_t gap_base, uint32_t gap_lane, const SliceBases &sb)
 {
+    constexpr int D = PF > 0 ? PF : 1;
     const uint8_t *fp = p.base + off;
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
     const uint32_t U = L ? (L + kUnit - 1) / kUnit : 1u;
@@ -170,8 +174,13 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
     const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
     const uint32_t b = (uint32_t)(uintptr_t)up & 3u;           // same for every unit of the frame
-    uint32_t nxt[kWords];
-    if (PF && R > 1) load_full<ALIGNED>(nxt, up, b);
+    constexpr uint64_t kStep = (uint64_t)G * kUnit;            // bytes between a lane's rounds
+    uint32_t nxt[D][kWords];
+    if (PF > 0) {
+#pragma unroll
+        for (int d = 0; d < D; d++)
+            if (R > 1u + d) load_full<ALIGNED>(nxt[d], up + d * kStep, b);
+    }
     uint32_t acc = 0;
     // Round 0's leading zero words (unit 0's front padding, lanes without a
     // unit) leave the zero register unchanged: the wave starts at the first
@@ -193,27 +202,44 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
         }
     }
-    for (uint32_t k = 1; k < R; k++, up += (uint64_t)G * kUnit) {
-        uint32_t w[kWords];
-        if (PF) {
-#pragma unroll
-            for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-            if (k + 1 < R) load_full<ALIGNED>(nxt, up + (uint64_t)G * kUnit, b);
-        } else {
+    // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, round 1).
+    const bool seed_spill = g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1;
+    if (PF == 0) {
+        for (uint32_t k = 1; k < R; k++, up += kStep) {
+            uint32_t w[kWords];
             load_full<ALIGNED>(w, up, b);
-        }
-        // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, k == 1).
-        if (k == 1 && g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1) w[0] ^= seed >> (8 * (kUnit - pad));
-        if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
+            if (k == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
+            if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
 #pragma unroll
-        for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
+            for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
+        }
+    } else {
+        // nxt[d] holds round k + d; once consumed it is refilled with round k + d + D.
+        for (uint32_t k = 1; k < R; k += D) {
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const uint32_t kk = k + d;
+                if (kk < R) {
+                    uint32_t w[kWords];
+#pragma unroll
+                    for (int i = 0; i < kWords; i++) w[i] = nxt[d][i];
+                    if (kk + D < R) load_full<ALIGNED>(nxt[d], up + (uint64_t)(kk + D - 1) * kStep, b);
+                    if (kk == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
+                    if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
+#pragma unroll
+                    for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
+                }
+            }
+        }
     }
-    // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j bytes.
+    // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j
+    // bytes (LDS nibble map: 8 lookups; or the bit matrix in SGPRs: 96 VALU).
 #pragma unroll
     for (int j = 0; (1 << j) < G; j++) {
         const uint32_t other = __shfl_xor(acc, 1 << j);
         const bool right = (g >> j) & 1;
-        acc = bitmatrix_apply(right ? other : acc, p.tree[j]) ^ (right ? acc : other);
+        const uint32_t left = right ? other : acc;
+        acc = (TREE_LDS ? tree_step(left, j) : bitmatrix_apply(left, p.tree[j])) ^ (right ? acc : other);
     }
     if (active && g == G - 1) {
         const uint32_t crc = acc ^ p.xorout;
@@ -238,11 +264,13 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 
 // Uniform geometry: persistent grid, each wave hashes 64/G frames per step.
 // ALIGNED: the host proved every unit start dword-aligned (strided batches).
-template <int G, bool PF, bool ALIGNED>
+template <int G, int PF, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
-    build_slice_tables(p.xtab);
-    if (G > 1) build_gap_table<32>(p.xgap[0], kLdsGap);
+    {
+        const int gi[1] = {ilog2(G)};
+        build_lds_tables<1, 32>(p.consts, gi, kLdsGap, ilog2(G));
+    }
     __syncthreads();
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
@@ -259,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         uint64_t off_n = 0;
         uint32_t L_n = 0;
         if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-        hash_frame<G, PF, 32, ALIGNED>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
+        hash_frame<G, PF, 32, ALIGNED, true>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
         f = fn;
         off = off_n;
         L = L_n;
@@ -425,13 +453,13 @@ __device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, 
     if (active) frame_desc(p, f, off, L);
 }
 
-template <int C, bool PF>
+template <int C, int PF>
 __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L,
                                            const SliceBases &sb)
 {
     constexpr int G = class_lanes(C);
     const int lane = threadIdx.x & 63;
-    hash_frame<G, PF, 16, false>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
+    hash_frame<G, PF, 16, false, false>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
 }
 
 // Ragged batches: persistent grid; waves pull items (64/G frames of one
@@ -446,14 +474,13 @@ __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, boo
 // static; item i + 2 is dequeued while item i hashes and item i + 1's
 // descriptors load, so neither latency is exposed. All four classes' gap maps
 // stay in LDS: waves never synchronise after the prologue.
-template <bool PF>
+template <int PF>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
-    build_slice_tables(p.xtab);
-    build_gap_table<16>(p.xgap[0], kLdsGap + 0u * 8192u);
-    build_gap_table<16>(p.xgap[1], kLdsGap + 1u * 8192u);
-    build_gap_table<16>(p.xgap[2], kLdsGap + 2u * 8192u);
-    build_gap_table<16>(p.xgap[3], kLdsGap + 3u * 8192u);
+    {
+        const int gi[kClasses] = {ilog2(class_lanes(0)), ilog2(class_lanes(1)), ilog2(class_lanes(2)), ilog2(class_lanes(3))};
+        build_lds_tables<kClasses, 16>(p.consts, gi, kLdsGap, 0);
+    }
     __syncthreads();
     const uint32_t *ctab = p.plan;
     const uint32_t items = ctab[12];

@@ -33,6 +33,7 @@ struct Ctx {
     size_t d_stage_cap = 0;
     uint8_t *d_small = nullptr;   // descriptors / outputs for host APIs
     size_t d_small_cap = 0;
+    uint32_t *d_consts = nullptr; // constant blob (tables, gap and merge maps)
 };
 Ctx g_ctx;
 thread_local std::string t_err;
@@ -69,6 +70,12 @@ val_status_t ensure_init(int device)
     VCRC_HIP(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(VAL_ERR_IO, "val_gpu_init: device is not gfx950");
     VCRC_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking), "hipStreamCreate");
+    {
+        uint32_t blob[kConstWords];
+        fill_const_blob(blob);
+        VCRC_HIP(hipMalloc((void **)&g_ctx.d_consts, sizeof blob), "hipMalloc(consts)");
+        VCRC_HIP(hipMemcpy(g_ctx.d_consts, blob, sizeof blob, hipMemcpyHostToDevice), "H2D consts");
+    }
     g_ctx.device = device;
     g_ctx.cus = prop.multiProcessorCount;
     g_ctx.ready = true;
@@ -110,28 +117,73 @@ uint32_t lanes_per_frame(uint32_t len)
     return f ? f : (uint32_t)class_lanes(length_class(len));
 }
 
-bool prefetch_on()
+// G for a uniform batch of n frames of len bytes: the class's G, doubled while
+// the batch would leave more than half of the machine's waves idle (a small
+// window spreads each frame over more lanes, so its serial chain is shorter),
+// up to 16 lanes and at most one 64-B unit per lane per round.
+uint32_t lanes_for_batch(uint32_t len, uint64_t n)
+{
+    uint32_t G = lanes_per_frame(len);
+    if (forced_lanes()) return G;
+    const uint64_t waves = (uint64_t)g_ctx.cus * kWavesPerBlock;
+    const uint64_t units = len ? (len + kUnit - 1) / kUnit : 1u;
+    while (G < 16 && 2u * G <= units && (n + 64 / G - 1) / (64 / G) * 2u <= waves) G *= 2;
+    return G;
+}
+
+bool valid_prefetch(int d) { return d == 0 || d == 1 || d == 2 || d == 4; }
+
+// Prefetch depth forced by val_gpu_set_prefetch or VAL_GPU_PREFETCH (-1 = none).
+int forced_prefetch()
 {
     static const int env_p = getenv("VAL_GPU_PREFETCH") ? atoi(getenv("VAL_GPU_PREFETCH")) : -1;
     const int forced = g_forced_prefetch.load(std::memory_order_relaxed);
-    if (forced >= 0) return forced != 0;
-    if (env_p >= 0) return env_p != 0;
-    return true;
+    if (forced >= 0) return forced;
+    return valid_prefetch(env_p) ? env_p : -1;
 }
+
+// Rounds kept in flight ahead of the one being hashed: 1 unless forced.
+// Measured on MI355X (profiles/r01_small_batches.log): issuing every round up
+// front (2 or 4 deep) lost 5-15% even on one-pass batches such as cfg2, since
+// the whole batch's requests then land before any wave can start hashing.
+int prefetch_depth()
+{
+    const int forced = forced_prefetch();
+    return forced >= 0 ? forced : 1;
+}
+
+// Merge-tree bit matrices (ragged kernel), computed once per process.
+struct TreeCols {
+    uint32_t col[kMaxTree][32];
+    TreeCols()
+    {
+        for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)kUnit << j, col[j]);
+    }
+};
 
 void fill_constants(FrameParams &p)
 {
-    for (int k = 0; k < 4; k++) p.xtab[k] = gf2_x8n((uint64_t)(k + 1));
-    for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)kUnit << j, p.tree[j]);
+    static const TreeCols tc;
+    p.consts = g_ctx.d_consts;
+    memcpy(p.tree, tc.col, sizeof p.tree);
+}
+
+template <int G, int PF>
+void launch_uniform_gp(bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
+{
+    if (aligned) hipLaunchKernelGGL((k_frames<G, PF, true>), grid, dim3(kBlock), 0, s, p);
+    else hipLaunchKernelGGL((k_frames<G, PF, false>), grid, dim3(kBlock), 0, s, p);
 }
 
 template <int G>
-void launch_uniform_g(bool pf, bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
+void launch_uniform_g(int pf, bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
 {
-    if (pf && aligned) hipLaunchKernelGGL((k_frames<G, true, true>), grid, dim3(kBlock), 0, s, p);
-    else if (pf) hipLaunchKernelGGL((k_frames<G, true, false>), grid, dim3(kBlock), 0, s, p);
-    else if (aligned) hipLaunchKernelGGL((k_frames<G, false, true>), grid, dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((k_frames<G, false, false>), grid, dim3(kBlock), 0, s, p);
+    switch (pf) {
+    case 0: launch_uniform_gp<G, 0>(aligned, grid, s, p); break;
+    case 2: launch_uniform_gp<G, 2>(aligned, grid, s, p); break;
+    case 4: launch_uniform_gp<G, 4>(aligned, grid, s, p); break;
+    default: launch_uniform_gp<G, 1>(aligned, grid, s, p); break;
+    }
 }
 
 // Every unit start is dword-aligned when frames are strided with a 4-multiple
@@ -147,12 +199,12 @@ bool units_dword_aligned(const FrameParams &p)
 val_status_t launch_uniform_one(FrameParams &p, uint32_t G, hipStream_t s)
 {
     fill_constants(p);
-    p.xgap[0] = gf2_x8n((uint64_t)(G - 1) * kUnit);
     const uint64_t groups_per_block = (uint64_t)kWavesPerBlock * (64 / G);
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
-    const bool pf = prefetch_on(), aligned = units_dword_aligned(p);
+    const bool aligned = units_dword_aligned(p);
+    const int pf = prefetch_depth();
     switch (G) {
     case 1: launch_uniform_g<1>(pf, aligned, grid, s, p); break;
     case 2: launch_uniform_g<2>(pf, aligned, grid, s, p); break;
@@ -225,7 +277,6 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
         hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, gcount, bstart, ctab);
         hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, bstart, blockoff, order);
         fill_constants(p);
-        for (int c = 0; c < kClasses; c++) p.xgap[c] = gf2_x8n((uint64_t)(class_lanes(c) - 1) * kUnit);
         p.order = order;
         p.plan = ctab;
         p.heads = heads;
@@ -233,8 +284,8 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
         const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
         const unsigned blocks = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>((uint64_t)g_ctx.cus, (max_items + kWavesPerBlock - 1) / kWavesPerBlock));
-        if (prefetch_on()) hipLaunchKernelGGL(k_frames_ragged<true>, dim3(blocks), dim3(kBlock), 0, s, p);
-        else hipLaunchKernelGGL(k_frames_ragged<false>, dim3(blocks), dim3(kBlock), 0, s, p);
+        if (forced_prefetch() == 0) hipLaunchKernelGGL(k_frames_ragged<0>, dim3(blocks), dim3(kBlock), 0, s, p);
+        else hipLaunchKernelGGL(k_frames_ragged<1>, dim3(blocks), dim3(kBlock), 0, s, p);
         e = hipGetLastError();
     }
     (void)hipFreeAsync(scratch, s);
@@ -247,7 +298,7 @@ val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
 {
     if (p.n == 0) return VAL_OK;
     if (p.off && typical_len == 0 && !forced_lanes()) return launch_ragged(p, s);
-    return launch_uniform(p, lanes_per_frame(typical_len ? typical_len : 16384u), s);
+    return launch_uniform(p, lanes_for_batch(typical_len ? typical_len : 16384u, p.n), s);
 }
 
 // NULL selects the HIP default (null) stream, as in every HIP API.
@@ -441,6 +492,8 @@ void val_gpu_shutdown(void)
     if (g_ctx.stream) (void)hipStreamSynchronize(g_ctx.stream);
     if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
     if (g_ctx.d_small) (void)hipFree(g_ctx.d_small);
+    if (g_ctx.d_consts) (void)hipFree(g_ctx.d_consts);
+    g_ctx.d_consts = nullptr;
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx.d_stage = g_ctx.d_small = nullptr;
     g_ctx.d_stage_cap = g_ctx.d_small_cap = 0;
@@ -469,9 +522,10 @@ val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes)
     return VAL_OK;
 }
 
-val_status_t val_gpu_set_prefetch(int on)
+val_status_t val_gpu_set_prefetch(int depth)
 {
-    g_forced_prefetch.store(on < 0 ? -1 : (on ? 1 : 0), std::memory_order_relaxed);
+    if (depth >= 0 && !valid_prefetch(depth)) return fail(VAL_ERR_INVALID_ARG, "prefetch depth must be -1, 0, 1, 2 or 4");
+    g_forced_prefetch.store(depth < 0 ? -1 : depth, std::memory_order_relaxed);
     return VAL_OK;
 }
 
