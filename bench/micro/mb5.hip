@@ -17,8 +17,8 @@
 __global__ __launch_bounds__(1024) void k_empty(uint32_t* out){ vcrc::s_lds[threadIdx.x] = threadIdx.x; __syncthreads(); if (vcrc::s_lds[(threadIdx.x + 1) & 1023] == 7777u) out[0] = 1; }
 
 __global__ __launch_bounds__(1024) void k_prologue(const vcrc::FrameParams p, uint32_t* out){
-  const int gi[1] = {6};
-  vcrc::build_lds_tables<1, 32>(p.consts, gi, vcrc::kLdsGap, 6);
+
+  vcrc::build_lds_tables(p.consts);
   __syncthreads();
   if (vcrc::s_lds[threadIdx.x * 37] == 7777u) out[0] = 1; }
 
@@ -45,7 +45,6 @@ int main(){
   static uint32_t blob[vcrc::kConstWords]; vcrc::fill_const_blob(blob);
   uint32_t* dc; CHECK(hipMalloc(&dc, sizeof blob)); CHECK(hipMemcpy(dc, blob, sizeof blob, hipMemcpyHostToDevice));
   p.consts = dc;
-  for (int j = 0; j < vcrc::kMaxTree; j++) gf2_shift_columns((uint64_t)vcrc::kUnit << j, p.tree[j]);
   p.base = d; p.stride = 1044; p.flen = 1040; p.last_len = 1040; p.seed0 = p.seed_rest = 0xFFFFFFFFu; p.xorout = 0xFFFFFFFFu;
   p.out_crc = out;
   for (int r = 0; r < 20; r++) { k_empty<<<cus, 1024>>>(out); CHECK(hipDeviceSynchronize()); }
@@ -58,6 +57,6 @@ int main(){
   for (uint32_t n : ns) {
     p.n = n;
     const unsigned blocks = (unsigned)((n + 15) / 16 < (uint32_t)cus ? (n + 15) / 16 : cus);
-    for (int r = 0; r < 20; r++) { hipLaunchKernelGGL((vcrc::k_frames<64, 1, true>), dim3(blocks), dim3(1024), 0, 0, p); CHECK(hipDeviceSynchronize()); }
+    for (int r = 0; r < 20; r++) { hipLaunchKernelGGL((vcrc::k_frames<64, 1>), dim3(blocks), dim3(1024), 0, 0, p); CHECK(hipDeviceSynchronize()); }
   }
   printf("done\n"); return 0; }

@@ -1,11 +1,15 @@
 """CPU model of the frame decomposition `hash_frame` runs on the GPU
 (val_protocol_amd/csrc/crc_kernels.hpp), checked against the oracle.
 
-The kernel cuts a frame's L bytes into U = ceil(L/64) units counted from the
-frame end, unit 0 front-padded with pad = 64U - L virtual zero bytes (free:
-the register is still 0 there), XORs the seed into frame bytes 0..3, hashes
-lane g's units u0+g+G*k (u0 = U - G*R) with a gap shift of 64(G-1) bytes
-between rounds, and merges the lanes with shifts of 64*2^j bytes. This
+The kernel anchors its unit grid at floor4(frame end): the first Lg = L - tb
+bytes (tb = (address of the frame end) mod 4) are cut into U = ceil(Lg/64)
+units counted from that point, so every unit is dword-aligned whatever the
+frame's byte alignment; unit 0 is front-padded with pad = 64U - Lg virtual
+zero bytes (free: the register is still 0 there). It XORs the seed into frame
+bytes 0..3, hashes lane g's units u0+g+G*k (u0 = U - G*R) with a gap shift of
+64(G-1) bytes between rounds, merges the lanes with shifts of 64*2^j bytes,
+then feeds the tb bytes past the grid with byte steps. Frames with Lg < 4 take
+the byte path. This
 restates that algebra byte-wise in Python (raw register updates via zlib), so
 the decomposition is proven on CPU for every length, alignment and lane
 count; the GPU tests prove the kernel.
@@ -50,12 +54,14 @@ def raw_update(reg: int, data: bytes) -> int:
 
 
 def model_frame(mem: bytes, fp: int, L: int, G: int, seed: int = M, xorout: int = M) -> int:
-    if L < 4:  # byte path
+    tb = min((fp + L) % 4, L)  # mem index = device address mod 4 (allocations are 4-aligned)
+    Lg = L - tb
+    if Lg < 4:  # byte path
         return raw_update(seed, mem[fp:fp + L]) ^ xorout
-    U = -(-L // 64)
+    U = -(-Lg // 64)
     R = -(-U // G)
-    pad = 64 * U - L
-    frame = bytearray(mem[fp:fp + L])
+    pad = 64 * U - Lg
+    frame = bytearray(mem[fp:fp + Lg])
     for j in range(4):  # seed XORed into frame bytes 0..3
         frame[j] ^= (seed >> (8 * j)) & 0xFF
     grid = bytes(pad) + bytes(frame)  # unit 0 front-padded with zeros
@@ -77,7 +83,7 @@ def model_frame(mem: bytes, fp: int, L: int, G: int, seed: int = M, xorout: int 
         sh = gf2_pow(X8, 64 * width)
         lanes = [gf2_mul(lanes[i], sh) ^ lanes[i + 1] for i in range(0, len(lanes), 2)]
         width *= 2
-    return lanes[0] ^ xorout
+    return raw_update(lanes[0], mem[fp + Lg:fp + L]) ^ xorout
 
 
 @pytest.mark.parametrize("G", [1, 2, 4, 16])

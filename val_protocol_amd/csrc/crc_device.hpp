@@ -2,14 +2,17 @@
 // LDS table layout, the slice-by-4 step, the gap step and the GF(2)
 // bit-matrix. Included by val_crc32_hip.hip only.
 //
-// LDS image (one per workgroup, 144 KiB, built in the prologue):
-//   [0, 128 KiB)      slice tables T3|T2 (pair 0) and T1|T0 (pair 1):
-//                     row = byte value * 256 B, half = 128 B, 32 bank replicas
-//                     of 4 B, so the 32 lanes of a half-wave read 32 banks.
-//   [128, 160 KiB)    gap maps as 8 nibble tables x 16 rows: one map with 32
-//                     replicas (uniform kernel, 16 KiB) or four maps with 16
-//                     replicas (ragged kernel, 4 x 8 KiB; lanes l and l+16
-//                     share a replica, so a gap lookup is at most 2-way).
+// LDS image (one per workgroup, built in the prologue from the device
+// constant blob):
+//   [0, 128 KiB)        slice tables T3|T2 (pair 0) and T1|T0 (pair 1):
+//                       row = byte value * 256 B, half = 128 B, 32 bank replicas
+//                       of 4 B, so the 32 lanes of a half-wave read 32 banks.
+//   [128 KiB, +6.5 KiB) 13 nibble maps of 512 B, one copy each: gap maps
+//                       "advance (G - 1) * 64 bytes" for G = 2^0..2^6, then
+//                       merge maps "advance 64 * 2^j bytes", j = 0..5. A map is
+//                       8 tables x 16 words; a lookup of nibble k reads one of
+//                       16 consecutive words, so lanes either share a word
+//                       (broadcast) or hit distinct banks: no replicas needed.
 // T_k[b] = b * x^(8(k+1)) mod P (T_0 = the classic table of the reference,
 // src/val_core.c:133-148).
 #pragma once
@@ -26,11 +29,12 @@ constexpr int kWords = kUnit / 4;
 constexpr int kBlock = 1024;           // threads per workgroup (16 waves, 1 workgroup per CU)
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kLdsS4 = 0;
-constexpr uint32_t kLdsGap = 131072;
-constexpr uint32_t kLdsWords = (131072 + 32768) / 4;  // 160 KiB: the whole LDS of a CU
+constexpr uint32_t kLdsMaps = 131072;
+constexpr uint32_t kNumMaps = 7 + 6;   // gap maps G = 2^0..2^6, merge maps j = 0..5
+constexpr uint32_t kLdsWords = (kLdsMaps + kNumMaps * 512) / 4;
 constexpr int kMaxTree = 6;            // log2(64 lanes)
 
-typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));  // unit loads are dword-aligned
 typedef uint32_t u32u __attribute__((aligned(1)));
 
 __shared__ uint32_t s_lds[kLdsWords];
@@ -72,18 +76,17 @@ __device__ __forceinline__ uint32_t byte_step(uint32_t c, uint32_t byte, const S
     return lds_read(tab_addr(c ^ byte, b.t0, 0)) ^ (c >> 8);
 }
 
-// Advance a register over the bytes other lanes own between two of this
-// lane's units: 8 nibble lookups in a gap map with REPL replicas per row,
-// based at `base` (byte address); lane_off = (lane % REPL) * 4.
-template <int REPL>
-__device__ __forceinline__ uint32_t gap_step(uint32_t a, uint32_t base, uint32_t lane_off)
+// Advance register a by the distance of the nibble map at byte address
+// `map`: 8 lookups (table k holds the images of n << 4k).
+__device__ __forceinline__ uint32_t map_apply(uint32_t a, uint32_t map)
 {
-    constexpr uint32_t kRow = REPL * 4, kTab = 16 * kRow;
     uint32_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) r ^= lds_read(base + (uint32_t)k * kTab + ((a >> (4 * k)) & 15u) * kRow + lane_off);
+    for (int k = 0; k < 8; k++) r ^= lds_read(map + (uint32_t)k * 64u + ((a >> (4 * k)) & 15u) * 4u);
     return r;
 }
+__host__ __device__ constexpr uint32_t gap_map(int gi) { return kLdsMaps + (uint32_t)gi * 512u; }
+__host__ __device__ constexpr uint32_t tree_map(int j) { return kLdsMaps + (7u + (uint32_t)j) * 512u; }
 
 // r = M v for a 32x32 GF(2) matrix given by its columns (wave-uniform, SGPRs).
 __device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *col)
@@ -101,31 +104,23 @@ __device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *
 //   [kConstGap,   +7*128)  nibble map "advance (G - 1) * 64 bytes" for G = 2^i,
 //                          entry k * 16 + n = image of n << 4k
 //   [kConstTree,  +6*128)  nibble map "advance 64 * 2^j bytes" (merge level j)
+// The maps are contiguous, in LDS order.
 constexpr uint32_t kConstSlice = 0, kConstGap = 1024, kConstTree = 1024 + 7 * 128;
 constexpr uint32_t kConstWords = kConstTree + kMaxTree * 128;
-constexpr uint32_t kLdsTree = kLdsGap + 16384;  // uniform kernel: 6 x 512 B merge maps after the gap map
 
-// Prologue: the LDS image is written in 16-B chunks, chunk c = r * 1024 + t
+// Prologue: the slice tables are written in 16-B chunks, chunk c = r * 1024 + t
 // for thread t, so the 64 lanes of a ds_write_b128 fill 1 KiB contiguously
 // (bank-conflict free; writing each thread's own 128-B table row instead put
-// all lanes 256 B apart and cost 3.4 us per launch). Every thread issues all
-// of its loads from the constant blob before it waits on any of them, so the
-// launch pays one memory latency.
-//   slice tables (128 KiB, 32 bank replicas): chunk c is row c >> 4 (pair =
-//     row >> 8, byte = row & 255), half (c >> 3) & 1 -> T_{3 - (2 pair + half)}[byte];
-//   gap maps: NMAPS maps of 16 x 8 rows (entry k * 16 + n) with REPL replicas,
-//     map m (G = 2^gi[m]) at base + m * 64 * REPL (= its size);
-//   merge maps: thread t < 128 * levels copies one word (one copy each: a
-//     lookup of nibble k reads 16 consecutive words, so lanes never share a bank).
-template <int NMAPS, int REPL>
-__device__ __forceinline__ void build_lds_tables(const uint32_t *consts, const int (&gi)[NMAPS], uint32_t base,
-                                                 int tree_levels)
+// all lanes 256 B apart and cost 3.4 us per launch). Chunk c is row c >> 4
+// (pair = row >> 8, byte = row & 255), half (c >> 3) & 1 ->
+// T_{3 - (2 pair + half)}[byte]. The maps are copied word for word. Every
+// thread issues all of its loads from the constant blob before it waits on any
+// of them, so the launch pays one memory latency.
+__device__ __forceinline__ void build_lds_tables(const uint32_t *consts)
 {
     const uint32_t t = threadIdx.x;
-    constexpr uint32_t kMapBytes = 128u * REPL * 4u;              // 128 entries x REPL words
-    constexpr uint32_t kGapChunks = NMAPS * kMapBytes / 16u;      // per workgroup
-    constexpr int kGapPer = (int)((kGapChunks + kBlock - 1) / kBlock);
-    uint32_t v[8], vg[kGapPer];
+    constexpr uint32_t kMapWords = kNumMaps * 128u;
+    uint32_t v[8], vm[2];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         const uint32_t c = (uint32_t)r * kBlock + t, row = c >> 4;
@@ -133,34 +128,18 @@ __device__ __forceinline__ void build_lds_tables(const uint32_t *consts, const i
         v[r] = consts[kConstSlice + (3u - slot) * 256u + (row & 255u)];
     }
 #pragma unroll
-    for (int r = 0; r < kGapPer; r++) {
-        const uint32_t c = (uint32_t)r * kBlock + t;
-        const uint32_t m = c / (kMapBytes / 16u), entry = (c % (kMapBytes / 16u)) / (REPL / 4u);
-        int g = gi[0];
-#pragma unroll
-        for (int q = 1; q < NMAPS; q++) g = m == (uint32_t)q ? gi[q] : g;
-        vg[r] = c < kGapChunks ? consts[kConstGap + (uint32_t)g * 128u + entry] : 0u;
+    for (int r = 0; r < 2; r++) {
+        const uint32_t i = (uint32_t)r * kBlock + t;
+        vm[r] = i < kMapWords ? consts[kConstGap + i] : 0u;
     }
-    const bool has_tree = t < (uint32_t)tree_levels * 128u;
-    const uint32_t vt = has_tree ? consts[kConstTree + t] : 0u;
     uint4 *lds4 = reinterpret_cast<uint4 *>(s_lds);
 #pragma unroll
     for (int r = 0; r < 8; r++) lds4[(kLdsS4 / 16u) + (uint32_t)r * kBlock + t] = make_uint4(v[r], v[r], v[r], v[r]);
 #pragma unroll
-    for (int r = 0; r < kGapPer; r++) {
-        const uint32_t c = (uint32_t)r * kBlock + t;
-        if (c < kGapChunks) lds4[base / 16u + c] = make_uint4(vg[r], vg[r], vg[r], vg[r]);
+    for (int r = 0; r < 2; r++) {
+        const uint32_t i = (uint32_t)r * kBlock + t;
+        if (i < kMapWords) s_lds[kLdsMaps / 4u + i] = vm[r];
     }
-    if (has_tree) s_lds[kLdsTree / 4 + t] = vt;
-}
-
-// Advance register a by 64 * 2^j bytes: 8 nibble lookups in merge map j.
-__device__ __forceinline__ uint32_t tree_step(uint32_t a, int j)
-{
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) r ^= lds_read(kLdsTree + (uint32_t)j * 512u + (uint32_t)k * 64u + ((a >> (4 * k)) & 15u) * 4u);
-    return r;
 }
 
 // Host: fill the constant blob (kConstWords u32).

@@ -54,59 +54,36 @@ struct FrameParams {
     const uint32_t *plan;    // ragged mode: class table {cstart[4], ccount[4], istart[5]}
     uint32_t *heads;         // ragged mode: 8 work-queue heads, 64 B apart, zero on entry
     const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
-    uint32_t tree[kMaxTree][32];  // columns of "advance 64 * 2^j bytes" (ragged kernel's merge)
 };
 
-// A full 64-B unit starting at byte address up, read with dword-aligned
-// loads only: 4 dwordx4 from floor4(up) plus one dword when up is not
-// 4-aligned (b = up & 3 = the same for every unit of a frame), then each word
-// funnel-shifted into place with v_alignbyte_b32. A dword-aligned load never
-// crosses a page, and device allocations are at least 4-aligned, so nothing
-// outside the buffer's pages is touched. Byte-misaligned dwordx4 loads would
-// cost ~60% of the ragged path's throughput (profiles/r01_ragged_pmc.txt).
-template <bool ALIGNED>
-__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up, uint32_t b)
+// A full 64-B unit at a dword-aligned address: four dwordx4 loads. Every
+// unit is dword-aligned by construction (hash_frame anchors the unit grid at
+// floor4(frame end)); a dword-aligned load never crosses a page, so nothing
+// outside the buffer's pages is touched.
+__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up)
 {
-    if (ALIGNED) {  // the host proved every unit dword-aligned (b == 0): plain loads
-#pragma unroll
-        for (int q = 0; q < kWords / 4; q++) {
-            const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
-            w[4 * q + 0] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-        return;
-    }
-    const uint8_t *a = up - b;
-    uint32_t d[kWords + 1];
 #pragma unroll
     for (int q = 0; q < kWords / 4; q++) {
-        const u32x4u v = *reinterpret_cast<const u32x4u *>(a + 16 * q);
-        d[4 * q + 0] = v.x;
-        d[4 * q + 1] = v.y;
-        d[4 * q + 2] = v.z;
-        d[4 * q + 3] = v.w;
+        const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
+        w[4 * q + 0] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
     }
-    d[kWords] = b ? *reinterpret_cast<const uint32_t *>(a + kUnit) : 0u;
-#pragma unroll
-    for (int i = 0; i < kWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], b);
 }
 
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
 // first unit, assembled word by word with the seed in frame bytes 0..3;
-// u < 0 nothing. L < 4 frames take the byte path (tiny).
-template <bool ALIGNED>
-__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const uint8_t *fp, uint32_t L, uint32_t pad,
+// u < 0 nothing. Lg = bytes on the unit grid; Lg < 4 frames take the byte path (tiny).
+__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const uint8_t *fp, uint32_t Lg, uint32_t pad,
                                            uint32_t seed, bool &tiny)
 {
     tiny = false;
     if (u > 0) {
-        const uint8_t *up = fp + (uint64_t)u * kUnit - pad;
-        load_full<ALIGNED>(w, up, (uint32_t)(uintptr_t)up & 3u);
+        load_full(w, fp + (uint64_t)u * kUnit - pad);
         // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
         if (u == 1 && pad > kUnit - 4) w[0] ^= seed >> (8 * (kUnit - pad));
-    } else if (u == 0 && L >= 4) {
+    } else if (u == 0 && Lg >= 4) {
 #pragma unroll
         for (int i = 0; i < kWords; i++) {
             const int q = 4 * i - (int)pad;  // frame offset of this word
@@ -161,25 +138,29 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // long batches (measured best); 2 or 4 when the whole batch is one pass of the
 // grid (small windows: every round's load is issued before the first returns,
 // so a wave pays one HBM latency instead of R - 1).
-template <int G, int PF, int REPL, bool ALIGNED, bool TREE_LDS>
+template <int G, int PF>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           uint32_t gap_base, uint32_t gap_lane, const SliceBases &sb)
+                                           const SliceBases &sb)
 {
     constexpr int D = PF > 0 ? PF : 1;
     const uint8_t *fp = p.base + off;
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
-    const uint32_t U = L ? (L + kUnit - 1) / kUnit : 1u;
+    // The unit grid ends at floor4(frame end), so every unit is dword-aligned
+    // whatever the frame's byte alignment; the tb <= 3 bytes past it are fed
+    // by byte steps after the merge.
+    const uint32_t tb = min((uint32_t)((uintptr_t)(fp + L) & 3u), L);
+    const uint32_t Lg = L - tb;
+    const uint32_t U = Lg ? (Lg + kUnit - 1) / kUnit : 1u;
     const uint32_t R = active ? (U + G - 1) / G : 0u;
-    const uint32_t pad = U * kUnit - L;
+    const uint32_t pad = U * kUnit - Lg;
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
     const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
-    const uint32_t b = (uint32_t)(uintptr_t)up & 3u;           // same for every unit of the frame
     constexpr uint64_t kStep = (uint64_t)G * kUnit;            // bytes between a lane's rounds
     uint32_t nxt[D][kWords];
     if (PF > 0) {
 #pragma unroll
         for (int d = 0; d < D; d++)
-            if (R > 1u + d) load_full<ALIGNED>(nxt[d], up + d * kStep, b);
+            if (R > 1u + d) load_full(nxt[d], up + d * kStep);
     }
     uint32_t acc = 0;
     // Round 0's leading zero words (unit 0's front padding, lanes without a
@@ -195,9 +176,9 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
         // unit; the register is still zero, so no gap step.
         uint32_t w[kWords];
         bool tiny;
-        load_unit0<ALIGNED>(w, u0, fp, L, pad, seed, tiny);
+        load_unit0(w, u0, fp, Lg, pad, seed, tiny);
         acc = s4_words_from(first, w, sb);
-        if (tiny) {  // L < 4: state of the few bytes straight from the seed
+        if (tiny) {  // Lg < 4: state of all L bytes straight from the seed
             acc = seed;
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
         }
@@ -207,9 +188,9 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     if (PF == 0) {
         for (uint32_t k = 1; k < R; k++, up += kStep) {
             uint32_t w[kWords];
-            load_full<ALIGNED>(w, up, b);
+            load_full(w, up);
             if (k == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
-            if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
+            if (G > 1) acc = map_apply(acc, gap_map(ilog2(G)));
 #pragma unroll
             for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
         }
@@ -223,9 +204,9 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
                     uint32_t w[kWords];
 #pragma unroll
                     for (int i = 0; i < kWords; i++) w[i] = nxt[d][i];
-                    if (kk + D < R) load_full<ALIGNED>(nxt[d], up + (uint64_t)(kk + D - 1) * kStep, b);
+                    if (kk + D < R) load_full(nxt[d], up + (uint64_t)(kk + D - 1) * kStep);
                     if (kk == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
-                    if (G > 1) acc = gap_step<REPL>(acc, gap_base, gap_lane);
+                    if (G > 1) acc = map_apply(acc, gap_map(ilog2(G)));
 #pragma unroll
                     for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
                 }
@@ -233,15 +214,17 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
         }
     }
     // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j
-    // bytes (LDS nibble map: 8 lookups; or the bit matrix in SGPRs: 96 VALU).
+    // bytes (LDS nibble map: 8 lookups, where a bit-matrix product costs 96 VALU).
 #pragma unroll
     for (int j = 0; (1 << j) < G; j++) {
         const uint32_t other = __shfl_xor(acc, 1 << j);
         const bool right = (g >> j) & 1;
         const uint32_t left = right ? other : acc;
-        acc = (TREE_LDS ? tree_step(left, j) : bitmatrix_apply(left, p.tree[j])) ^ (right ? acc : other);
+        acc = map_apply(left, tree_map(j)) ^ (right ? acc : other);
     }
     if (active && g == G - 1) {
+        if (Lg >= 4)  // the bytes past the unit grid (tiny frames already fed all L)
+            for (uint32_t i = Lg; i < L; i++) acc = byte_step(acc, fp[i], sb);
         const uint32_t crc = acc ^ p.xorout;
         if (p.out_crc) p.out_crc[f] = crc;
         if (p.verify) {
@@ -263,19 +246,14 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 }
 
 // Uniform geometry: persistent grid, each wave hashes 64/G frames per step.
-// ALIGNED: the host proved every unit start dword-aligned (strided batches).
-template <int G, int PF, bool ALIGNED>
+template <int G, int PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
-    {
-        const int gi[1] = {ilog2(G)};
-        build_lds_tables<1, 32>(p.consts, gi, kLdsGap, ilog2(G));
-    }
+    build_lds_tables(p.consts);
     __syncthreads();
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
-    const uint32_t lo4 = (uint32_t)(lane & 31) << 2;
-    const SliceBases sb = slice_bases(lo4);
+    const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
     const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
     // Descriptors of the next frame group are fetched while this one hashes.
@@ -287,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         uint64_t off_n = 0;
         uint32_t L_n = 0;
         if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-        hash_frame<G, PF, 32, ALIGNED, true>(p, f, f < p.n, off, L, lane % G, kLdsGap, lo4, sb);
+        hash_frame<G, PF>(p, f, f < p.n, off, L, lane % G, sb);
         f = fn;
         off = off_n;
         L = L_n;
@@ -459,7 +437,7 @@ __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, boo
 {
     constexpr int G = class_lanes(C);
     const int lane = threadIdx.x & 63;
-    hash_frame<G, PF, 16, false, false>(p, f, active, off, L, lane % G, kLdsGap + (uint32_t)C * 8192u, (uint32_t)(lane & 15) << 2, sb);
+    hash_frame<G, PF>(p, f, active, off, L, lane % G, sb);
 }
 
 // Ragged batches: persistent grid; waves pull items (64/G frames of one
@@ -477,10 +455,7 @@ __device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, boo
 template <int PF>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
-    {
-        const int gi[kClasses] = {ilog2(class_lanes(0)), ilog2(class_lanes(1)), ilog2(class_lanes(2)), ilog2(class_lanes(3))};
-        build_lds_tables<kClasses, 16>(p.consts, gi, kLdsGap, 0);
-    }
+    build_lds_tables(p.consts);
     __syncthreads();
     const uint32_t *ctab = p.plan;
     const uint32_t items = ctab[12];

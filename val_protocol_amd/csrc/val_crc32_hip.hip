@@ -152,48 +152,17 @@ int prefetch_depth()
     return forced >= 0 ? forced : 1;
 }
 
-// Merge-tree bit matrices (ragged kernel), computed once per process.
-struct TreeCols {
-    uint32_t col[kMaxTree][32];
-    TreeCols()
-    {
-        for (int j = 0; j < kMaxTree; j++) gf2_shift_columns((uint64_t)kUnit << j, col[j]);
-    }
-};
-
-void fill_constants(FrameParams &p)
-{
-    static const TreeCols tc;
-    p.consts = g_ctx.d_consts;
-    memcpy(p.tree, tc.col, sizeof p.tree);
-}
-
-template <int G, int PF>
-void launch_uniform_gp(bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
-{
-    if (aligned) hipLaunchKernelGGL((k_frames<G, PF, true>), grid, dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((k_frames<G, PF, false>), grid, dim3(kBlock), 0, s, p);
-}
+void fill_constants(FrameParams &p) { p.consts = g_ctx.d_consts; }
 
 template <int G>
-void launch_uniform_g(int pf, bool aligned, dim3 grid, hipStream_t s, const FrameParams &p)
+void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
 {
     switch (pf) {
-    case 0: launch_uniform_gp<G, 0>(aligned, grid, s, p); break;
-    case 2: launch_uniform_gp<G, 2>(aligned, grid, s, p); break;
-    case 4: launch_uniform_gp<G, 4>(aligned, grid, s, p); break;
-    default: launch_uniform_gp<G, 1>(aligned, grid, s, p); break;
+    case 0: hipLaunchKernelGGL((k_frames<G, 0>), grid, dim3(kBlock), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((k_frames<G, 2>), grid, dim3(kBlock), 0, s, p); break;
+    case 4: hipLaunchKernelGGL((k_frames<G, 4>), grid, dim3(kBlock), 0, s, p); break;
+    default: hipLaunchKernelGGL((k_frames<G, 1>), grid, dim3(kBlock), 0, s, p); break;
     }
-}
-
-// Every unit start is dword-aligned when frames are strided with a 4-multiple
-// stride and (base + L) is 4-aligned for both lengths: a unit starts at
-// base + f*stride + L - 64k. Descriptor batches take the realigning loads.
-bool units_dword_aligned(const FrameParams &p)
-{
-    if (p.off) return false;
-    const uintptr_t b = (uintptr_t)p.base;
-    return p.stride % 4 == 0 && (b + p.flen) % 4 == 0 && (b + p.last_len) % 4 == 0;
 }
 
 val_status_t launch_uniform_one(FrameParams &p, uint32_t G, hipStream_t s)
@@ -203,16 +172,15 @@ val_status_t launch_uniform_one(FrameParams &p, uint32_t G, hipStream_t s)
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)g_ctx.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
-    const bool aligned = units_dword_aligned(p);
     const int pf = prefetch_depth();
     switch (G) {
-    case 1: launch_uniform_g<1>(pf, aligned, grid, s, p); break;
-    case 2: launch_uniform_g<2>(pf, aligned, grid, s, p); break;
-    case 4: launch_uniform_g<4>(pf, aligned, grid, s, p); break;
-    case 8: launch_uniform_g<8>(pf, aligned, grid, s, p); break;
-    case 16: launch_uniform_g<16>(pf, aligned, grid, s, p); break;
-    case 32: launch_uniform_g<32>(pf, aligned, grid, s, p); break;
-    case 64: launch_uniform_g<64>(pf, aligned, grid, s, p); break;
+    case 1: launch_uniform_g<1>(pf, grid, s, p); break;
+    case 2: launch_uniform_g<2>(pf, grid, s, p); break;
+    case 4: launch_uniform_g<4>(pf, grid, s, p); break;
+    case 8: launch_uniform_g<8>(pf, grid, s, p); break;
+    case 16: launch_uniform_g<16>(pf, grid, s, p); break;
+    case 32: launch_uniform_g<32>(pf, grid, s, p); break;
+    case 64: launch_uniform_g<64>(pf, grid, s, p); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
