@@ -14,4 +14,6 @@ for i, s in enumerate(specs):
     grp = rows[i * reps * per:(i + 1) * reps * per]
     calls = [grp[j * per:(j + 1) * per] for j in range(reps)]
     d = [(c[-1][1] - c[0][0]) / 1000 for c in calls]
-    print(f"{s:16s} kernels/call={per} med={median(d):8.2f} us min={min(d):8.2f} us  {calls[0][0][2][:40]}")
+    parts = " ".join(f"{c[2].split('(')[0].split('::')[-1][:18]}={median([(x[j][1] - x[j][0]) / 1000 for x in calls]):.1f}"
+                     for j, c in enumerate(calls[0]))
+    print(f"{s:16s} kernels/call={per} med={median(d):8.2f} us min={min(d):8.2f} us  {parts}")

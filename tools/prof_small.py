@@ -20,10 +20,13 @@ for spec in sys.argv[2:]:
     if name not in cache:
         cache[name] = workload(name, dev)
     w, nbytes = cache[name]
-    out = torch.empty(w["n"], dtype=torch.int32, device=dev)
+    out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
     vc.set_geometry(int(G), int(PF))
     for _ in range(reps):
-        vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
+        if "off" in w:
+            vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=w["len_hint"])
+        else:
+            vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
         torch.cuda.synchronize()
     print(spec, nbytes, flush=True)
 vc.set_geometry()

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Minimal profiling target: builds the cfg workload once and launches the
-frames kernel `reps` times (run under rocprofv3). Usage: prof_target.py [cfg] [reps] [verify]"""
+frames kernel `reps` times (run under rocprofv3). Usage: prof_target.py [cfg] [reps] [verify] [nohdr]"""
 import os
 import sys
 
@@ -12,12 +12,13 @@ import val_protocol_amd.crc as vc  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-verify = len(sys.argv) > 3 and sys.argv[3] == "verify"
+verify = "verify" in sys.argv[3:]
+nohdr = "nohdr" in sys.argv[3:]  # diagnostic: no header_crc output
 dev = torch.device("cuda:0")
 vc.init(0)
 n, payload, explicit, header = bench.CONFIGS[cfg]
 crc = torch.empty(n, dtype=torch.int32, device=dev)
-hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
+hdr = torch.empty(n, dtype=torch.int32, device=dev) if header and not nohdr else None
 if cfg == "cfg5":  # ragged descriptor batch, binned on the device (len_hint 0)
     flat, d_off, d_len = bench.make_ragged_frames(torch, dev, n, seed=1234)  # = bench.py rank 0
     kw = dict(off=d_off, length=d_len, len_hint=0)

@@ -138,11 +138,15 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // long batches (measured best); 2 or 4 when the whole batch is one pass of the
 // grid (small windows: every round's load is issued before the first returns,
 // so a wave pays one HBM latency instead of R - 1).
-template <int G, int PF>
+// GT = 0: G is the runtime value Gr (the ragged kernel: one code path for
+// every length class, half the registers of four inlined instances).
+template <int GT, int PF>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           const SliceBases &sb)
+                                           const SliceBases &sb, int Gr = GT)
 {
     constexpr int D = PF > 0 ? PF : 1;
+    const int G = GT ? GT : Gr;
+    const uint32_t gmap = gap_map(GT ? ilog2(GT) : __builtin_ctz((unsigned)Gr));
     const uint8_t *fp = p.base + off;
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
     // The unit grid ends at floor4(frame end), so every unit is dword-aligned
@@ -155,7 +159,7 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     const uint32_t pad = U * kUnit - Lg;
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
     const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
-    constexpr uint64_t kStep = (uint64_t)G * kUnit;            // bytes between a lane's rounds
+    const uint64_t kStep = (uint64_t)G * kUnit;                // bytes between a lane's rounds
     uint32_t nxt[D][kWords];
     if (PF > 0) {
 #pragma unroll
@@ -171,6 +175,19 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
     first = __builtin_amdgcn_readfirstlane(first);
+    // header_crc: by the lane holding unit 0, while the frame's first line is
+    // being read anyway (read after the merge, the line had left the caches:
+    // +0.4% HBM traffic on cfg3).
+    if (R > 0 && u0 == 0 && p.out_hdr) {
+        uint32_t h = seed;
+        if (L >= 8) {
+            h = s4_step(h, ld32(fp), sb);
+            h = s4_step(h, ld32(fp + 4), sb);
+        } else {
+            for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
+        }
+        p.out_hdr[f] = h ^ p.xorout;
+    }
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
@@ -190,7 +207,7 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             uint32_t w[kWords];
             load_full(w, up);
             if (k == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
-            if (G > 1) acc = map_apply(acc, gap_map(ilog2(G)));
+            if (G > 1) acc = map_apply(acc, gmap);
 #pragma unroll
             for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
         }
@@ -206,7 +223,7 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
                     for (int i = 0; i < kWords; i++) w[i] = nxt[d][i];
                     if (kk + D < R) load_full(nxt[d], up + (uint64_t)(kk + D - 1) * kStep);
                     if (kk == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
-                    if (G > 1) acc = map_apply(acc, gap_map(ilog2(G)));
+                    if (G > 1) acc = map_apply(acc, gmap);
 #pragma unroll
                     for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
                 }
@@ -216,7 +233,8 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j
     // bytes (LDS nibble map: 8 lookups, where a bit-matrix product costs 96 VALU).
 #pragma unroll
-    for (int j = 0; (1 << j) < G; j++) {
+    for (int j = 0; j < kMaxTree; j++) {
+        if ((1 << j) >= G) break;
         const uint32_t other = __shfl_xor(acc, 1 << j);
         const bool right = (g >> j) & 1;
         const uint32_t left = right ? other : acc;
@@ -232,16 +250,6 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
             if (!good && p.nbad) atomicAdd(p.nbad, 1u);
         }
-    }
-    if (active && g == 0 && p.out_hdr) {
-        uint32_t h = seed;
-        if (L >= 8) {
-            h = s4_step(h, ld32(fp), sb);
-            h = s4_step(h, ld32(fp + 4), sb);
-        } else {
-            for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
-        }
-        p.out_hdr[f] = h ^ p.xorout;
     }
 }
 
@@ -431,15 +439,6 @@ __device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, 
     if (active) frame_desc(p, f, off, L);
 }
 
-template <int C, int PF>
-__device__ __forceinline__ void hash_class(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L,
-                                           const SliceBases &sb)
-{
-    constexpr int G = class_lanes(C);
-    const int lane = threadIdx.x & 63;
-    hash_frame<G, PF>(p, f, active, off, L, lane % G, sb);
-}
-
 // Ragged batches: persistent grid; waves pull items (64/G frames of one
 // class, longest first) from a work queue, so the launch ends about one item
 // after the bytes run out (longest-processing-time-first: a static cyclic deal
@@ -486,12 +485,8 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
             nxt = ragged_item(ctab, it_n);
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
-        switch (cur.c) {
-        case 3: hash_class<3, PF>(p, f, active, off, L, sb); break;
-        case 2: hash_class<2, PF>(p, f, active, off, L, sb); break;
-        case 1: hash_class<1, PF>(p, f, active, off, L, sb); break;
-        default: hash_class<0, PF>(p, f, active, off, L, sb); break;
-        }
+        const int G = class_lanes(cur.c);
+        hash_frame<0, PF>(p, f, active, off, L, lane & (G - 1), sb, G);
         if (it_n >= items) break;
         it = it_n;
         it_n = part + P * (__builtin_amdgcn_readfirstlane(k_nn) + 2u * nwp);
