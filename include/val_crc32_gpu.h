@@ -94,12 +94,28 @@ uint64_t val_crc32_region_scratch_bytes(uint64_t len);
 
 /* ---- batch frames, host memory (synchronous; H2D + kernel + D2H) --------
  * base_len bounds every frame: off[i] + len[i] (+4 for verify) <= base_len,
- * else VAL_ERR_INVALID_ARG. off/len NULL = strided mode as above.        */
+ * else VAL_ERR_INVALID_ARG. off/len NULL = strided mode as above.
+ * Frames travel H2D in chunks of whole frames on a copy stream while the
+ * previous chunk is hashed (descriptor batches chunk when their offsets are
+ * non-decreasing). A pinned `base` (val_gpu_host_alloc, hipHostMalloc or
+ * hipHostRegister) is copied by DMA in place; pageable memory goes through
+ * two internal pinned bounce buffers (host memcpy, up to 8 threads).
+ * Mixed-length descriptor batches take the device-binned ragged path.   */
 val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                                    uint64_t stride, uint32_t flen, uint32_t n, uint32_t *crc, uint32_t *hdr);
 val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
                                           const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint8_t *ok,
                                           uint32_t *nbad);
+
+/* ---- pinned host staging ------------------------------------------------
+ * Page-locked host memory for frame windows (e.g. the TX window staging
+ * buffer of INTEGRATION.md section 3): the *_frames_host calls copy it by DMA
+ * without a bounce. NULL on failure (val_gpu_last_error). */
+void *val_gpu_host_alloc(size_t bytes);
+void val_gpu_host_free(void *p);
+/* Wire bytes per H2D chunk of the *_frames_host calls; 0 = default (64 MiB).
+ * Device memory use is two chunks. Speed and memory only; results never change. */
+val_status_t val_gpu_set_host_chunk_bytes(size_t bytes);
 
 /* ---- introspection for benchmarks ---------------------------------------
  * Lanes per frame the library would pick for a given typical length. */

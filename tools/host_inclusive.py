@@ -61,7 +61,26 @@ def main():
     rows = host[torch.from_numpy(idx)].numpy().reshape(-1)
     ok = np.array_equal(hcrc.numpy().view(np.uint32)[idx], _oracle.frames_strided(rows, stride, flen, idx.size))
     print(f"host-inclusive cfg3 ({n} frames, pinned, {chunk}-frame chunks, 2 streams): {gib:.1f} GiB/s CRC input, "
-          f"{h2d:.1f} GB/s H2D wire bytes, {dt * 1e3:.1f} ms per pass, parity={ok}")
+          f"{h2d:.1f} GB/s H2D wire bytes, {dt * 1e3:.1f} ms per pass, parity={ok}", flush=True)
+
+    # The product's own host API (C ABI, native chunked pipeline): pinned
+    # buffer from val_gpu_host_alloc (DMA in place) and a pageable copy
+    # (pinned bounce buffers, host memcpy threads).
+    want = hcrc.numpy().view(np.uint32).copy()
+    pb = vc.PinnedBuffer(n * stride)
+    pb.array[:] = host.numpy().reshape(-1)
+    pageable = np.array(host.numpy().reshape(-1))
+    del host
+    for name, arr in (("pinned (val_gpu_host_alloc)", pb.array), ("pageable", pageable)):
+        vc.frames_host(arr, stride=stride, flen=flen, n=n)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = vc.frames_host(arr, stride=stride, flen=flen, n=n)
+        dt = (time.perf_counter() - t0) / reps
+        print(f"C-ABI val_crc32_frames_host cfg3 ({n} frames, {name}): {n * flen / dt / (1 << 30):.1f} GiB/s CRC input, "
+              f"{n * stride / dt / 1e9:.1f} GB/s wire, {dt * 1e3:.1f} ms per call, parity={np.array_equal(got, want)}",
+              flush=True)
+    pb.free()
 
 
 if __name__ == "__main__":

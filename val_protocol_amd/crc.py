@@ -42,7 +42,8 @@ EXPORTS = (
     "val_crc32_frames_dev", "val_crc32_verify_frames_dev", "val_crc32_region_dev",
     "val_crc32_region_scratch_bytes", "val_crc32_frames_host", "val_crc32_verify_frames_host",
     "val_serialize_frame_header", "val_deserialize_frame_header", "val_frame_data_batch",
-    "val_frame_put_trailers", "val_frame_scan",
+    "val_frame_put_trailers", "val_frame_scan", "val_gpu_host_alloc", "val_gpu_host_free",
+    "val_gpu_set_host_chunk_bytes",
 )
 
 
@@ -93,6 +94,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_frame_data_batch", i32, _vp, _vp, _vp, _vp, _vp, u32, _vp, sz, _vp, _vp, ctypes.POINTER(sz))
     fn("val_frame_put_trailers", None, _vp, _vp, _vp, _vp, u32)
     fn("val_frame_scan", i32, _vp, sz, sz, u32, _vp, _vp, ctypes.POINTER(u32), ctypes.POINTER(sz))
+    fn("val_gpu_host_alloc", _vp, sz)
+    fn("val_gpu_host_free", None, _vp)
+    fn("val_gpu_set_host_chunk_bytes", i32, sz)
 
 
 def lib() -> ctypes.CDLL:
@@ -263,6 +267,36 @@ def region(buf, state_in: int = 0xFFFFFFFF, out=None, stream=None):
 
 
 # ---- host-memory batches ----------------------------------------------------
+class PinnedBuffer:
+    """Page-locked host bytes from val_gpu_host_alloc, viewed as a numpy
+    uint8 array (`.array`); freed with `.free()` or on garbage collection."""
+
+    def __init__(self, nbytes: int):
+        self._lib = lib()
+        self._ptr = self._lib.val_gpu_host_alloc(max(1, nbytes))
+        if not self._ptr:
+            raise ValError(int(VAL_ERR_NO_MEMORY), "val_gpu_host_alloc", last_error())
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, nbytes)).from_address(self._ptr))[:nbytes]
+
+    def free(self) -> None:
+        if self._ptr:
+            self.array = None
+            self._lib.val_gpu_host_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def set_host_chunk_bytes(nbytes: int) -> None:
+    """Wire bytes per H2D chunk of the host-memory calls (0 = default 64 MiB)."""
+    _check(lib().val_gpu_set_host_chunk_bytes(nbytes), "val_gpu_set_host_chunk_bytes")
+
+
 def frames_host(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
                 stride: int = 0, flen: int = 0, n: Optional[int] = None, header: bool = False):
     base = np.ascontiguousarray(base, dtype=np.uint8)

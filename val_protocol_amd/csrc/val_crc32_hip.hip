@@ -13,6 +13,8 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "crc_kernels.hpp"
 #include "val_crc32_gpu.h"
@@ -34,6 +36,15 @@ struct Ctx {
     uint8_t *d_small = nullptr;   // descriptors / outputs for host APIs
     size_t d_small_cap = 0;
     uint32_t *d_consts = nullptr; // constant blob (tables, gap and merge maps)
+    // host-API pipeline: frames go H2D in chunks on `copy` while the previous
+    // chunk is hashed on `stream` (two device slots; two pinned bounce
+    // buffers for pageable inputs)
+    hipStream_t copy = nullptr;
+    hipEvent_t h2d_done[2] = {}, kern_done[2] = {};
+    uint8_t *d_slot[2] = {};
+    size_t d_slot_cap[2] = {};
+    uint8_t *h_bounce[2] = {};
+    size_t h_bounce_cap[2] = {};
 };
 Ctx g_ctx;
 thread_local std::string t_err;
@@ -70,6 +81,11 @@ val_status_t ensure_init(int device)
     VCRC_HIP(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return fail(VAL_ERR_IO, "val_gpu_init: device is not gfx950");
     VCRC_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking), "hipStreamCreate");
+    VCRC_HIP(hipStreamCreateWithFlags(&g_ctx.copy, hipStreamNonBlocking), "hipStreamCreate(copy)");
+    for (int i = 0; i < 2; i++) {
+        VCRC_HIP(hipEventCreateWithFlags(&g_ctx.h2d_done[i], hipEventDisableTiming), "hipEventCreate");
+        VCRC_HIP(hipEventCreateWithFlags(&g_ctx.kern_done[i], hipEventDisableTiming), "hipEventCreate");
+    }
     {
         uint32_t blob[kConstWords];
         fill_const_blob(blob);
@@ -377,6 +393,63 @@ uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t l
     return out;
 }
 
+std::atomic<size_t> g_host_chunk{0};
+constexpr size_t kDefaultHostChunk = 64u << 20;
+
+size_t host_chunk_bytes()
+{
+    const size_t c = g_host_chunk.load(std::memory_order_relaxed);
+    return c ? c : kDefaultHostChunk;
+}
+
+// Pinned (page-locked) host memory is copied by DMA straight from the
+// caller's buffer; pageable memory goes through pinned bounce buffers.
+bool is_pinned(const void *p)
+{
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+// memcpy with up to 8 host threads (one pinned bounce chunk).
+void parallel_copy(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>({8u, hw, (n + (4u << 20) - 1) / (4u << 20)});
+    if (nt <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (size_t t = 0; t < nt; t++) {
+        const size_t lo = t * per, hi = std::min(n, lo + per);
+        if (lo < hi) th.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
+    }
+    for (auto &x : th) x.join();
+}
+
+val_status_t grow_pinned(uint8_t **buf, size_t *cap, size_t need)
+{
+    if (*cap >= need) return VAL_OK;
+    if (*buf) (void)hipHostFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    hipError_t e = hipHostMalloc((void **)buf, need, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(VAL_ERR_NO_MEMORY, "hipHostMalloc(bounce)", e);
+    *cap = need;
+    return VAL_OK;
+}
+
+// Host-memory batches: descriptors H2D once, then frames in chunks of whole
+// frames (<= host_chunk_bytes of wire span each) through two device slots:
+// chunk c's H2D on the copy stream overlaps chunk c-1's kernel on the compute
+// stream; the outputs come back D2H once at the end. Descriptor batches are
+// chunked when their offsets are non-decreasing (a packed stream); otherwise
+// the whole span is one chunk.
 val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                          uint64_t stride, uint32_t flen, uint32_t n, int verify, uint32_t *crc, uint32_t *hdr,
                          uint8_t *ok, uint32_t *nbad)
@@ -384,22 +457,23 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     if (!base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
     if ((off == nullptr) != (len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
     const uint64_t tail = verify ? 4u : 0u;
-    uint64_t span = 0, len_sum = 0;
+    uint32_t lmin = UINT32_MAX, lmax = 0;
+    bool monotone = true;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t o = off ? off[i] : (uint64_t)i * stride;
         const uint64_t l = len ? len[i] : flen;
         if (o > base_len || l + tail > base_len - o) return fail(VAL_ERR_INVALID_ARG, "frame overruns the buffer");
-        span = std::max(span, o + l + tail);
-        len_sum += l;
+        lmin = std::min<uint32_t>(lmin, (uint32_t)l);
+        lmax = std::max<uint32_t>(lmax, (uint32_t)l);
+        if (off && i && off[i] < off[i - 1]) monotone = false;
     }
     val_status_t st = bind_thread();
     if (st != VAL_OK) return st;
     std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
     const size_t desc_bytes = off ? (size_t)n * 12u : 0u;
     const size_t out_bytes = (size_t)n * 9u + 16u;
-    if ((st = grow(&g_ctx.d_stage, &g_ctx.d_stage_cap, span ? span : 1)) != VAL_OK) return st;
     if ((st = grow(&g_ctx.d_small, &g_ctx.d_small_cap, desc_bytes + out_bytes + 64)) != VAL_OK) return st;
-    hipStream_t s = g_ctx.stream;
+    hipStream_t s = g_ctx.stream, cs = g_ctx.copy;
     uint8_t *sm = g_ctx.d_small;
     uint64_t *d_off = off ? reinterpret_cast<uint64_t *>(sm) : nullptr;
     uint32_t *d_len = off ? reinterpret_cast<uint32_t *>(sm + (size_t)n * 8u) : nullptr;
@@ -407,29 +481,82 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     uint32_t *d_hdr = d_crc + n;
     uint32_t *d_nbad = d_hdr + n;
     uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_nbad + 4);
-    if (span) VCRC_HIP(hipMemcpyAsync(g_ctx.d_stage, base, span, hipMemcpyHostToDevice, s), "H2D frames");
     if (off) {
         VCRC_HIP(hipMemcpyAsync(d_off, off, (size_t)n * 8u, hipMemcpyHostToDevice, s), "H2D off");
         VCRC_HIP(hipMemcpyAsync(d_len, len, (size_t)n * 4u, hipMemcpyHostToDevice, s), "H2D len");
     }
     VCRC_HIP(hipMemsetAsync(d_nbad, 0, 4, s), "memset");
-    FrameParams p{};
-    p.base = g_ctx.d_stage;
-    p.off = d_off;
-    p.len = d_len;
-    p.stride = stride;
-    p.flen = flen;
-    p.last_len = flen;
-    p.n = n;
-    p.seed0 = p.seed_rest = 0xFFFFFFFFu;
-    p.xorout = 0xFFFFFFFFu;
-    p.out_crc = crc ? d_crc : nullptr;
-    p.out_hdr = hdr ? d_hdr : nullptr;
-    p.verify = verify ? 1u : 0u;
-    p.out_ok = ok ? d_ok : nullptr;
-    p.nbad = d_nbad;
-    const uint32_t typical = n ? (uint32_t)std::min<uint64_t>(len_sum / n, 0xFFFFFFFFu) : 0u;
-    if ((st = launch_frames(p, typical, s)) != VAL_OK) return st;
+    // chunks of whole frames [i0, i1) covering wire bytes [lo, hi)
+    const size_t cap = host_chunk_bytes();
+    struct Chunk {
+        uint32_t i0, i1;
+        uint64_t lo, hi;
+    };
+    std::vector<Chunk> chunks;
+    auto o_of = [&](uint32_t i) { return off ? off[i] : (uint64_t)i * stride; };
+    auto e_of = [&](uint32_t i) { return o_of(i) + (len ? len[i] : flen) + tail; };
+    if (off && !monotone) {
+        Chunk c{0, n, UINT64_MAX, 0};
+        for (uint32_t i = 0; i < n; i++) {
+            c.lo = std::min(c.lo, o_of(i));
+            c.hi = std::max(c.hi, e_of(i));
+        }
+        if (n) chunks.push_back(c);
+    } else {
+        for (uint32_t i = 0; i < n;) {
+            Chunk c{i, i + 1, o_of(i), e_of(i)};
+            while (c.i1 < n && std::max(c.hi, e_of(c.i1)) - c.lo <= cap) c.hi = std::max(c.hi, e_of(c.i1++));
+            chunks.push_back(c);
+            i = c.i1;
+        }
+    }
+    size_t slot_need = 1;
+    for (const Chunk &c : chunks) slot_need = std::max<size_t>(slot_need, (size_t)(c.hi - c.lo));
+    const bool pinned = n && is_pinned(base);
+    for (int k = 0; k < 2; k++) {
+        if ((st = grow(&g_ctx.d_slot[k], &g_ctx.d_slot_cap[k], slot_need)) != VAL_OK) return st;
+        if (!pinned && n && (st = grow_pinned(&g_ctx.h_bounce[k], &g_ctx.h_bounce_cap[k], slot_need)) != VAL_OK)
+            return st;
+    }
+    // no slot may be refilled before the previous call's kernels finished with it
+    VCRC_HIP(hipEventRecord(g_ctx.kern_done[0], s), "hipEventRecord");
+    VCRC_HIP(hipEventRecord(g_ctx.kern_done[1], s), "hipEventRecord");
+    VCRC_HIP(hipEventRecord(g_ctx.h2d_done[0], cs), "hipEventRecord");
+    VCRC_HIP(hipEventRecord(g_ctx.h2d_done[1], cs), "hipEventRecord");
+    const uint32_t hint = (off && lmin != lmax) ? 0u : lmax;
+    for (size_t c = 0; c < chunks.size(); c++) {
+        const Chunk &ch = chunks[c];
+        const int k = (int)(c & 1);
+        const size_t bytes = (size_t)(ch.hi - ch.lo);
+        VCRC_HIP(hipStreamWaitEvent(cs, g_ctx.kern_done[k], 0), "hipStreamWaitEvent");
+        if (pinned) {
+            VCRC_HIP(hipMemcpyAsync(g_ctx.d_slot[k], base + ch.lo, bytes, hipMemcpyHostToDevice, cs), "H2D frames");
+        } else {
+            VCRC_HIP(hipEventSynchronize(g_ctx.h2d_done[k]), "hipEventSynchronize");  // bounce k drained
+            parallel_copy(g_ctx.h_bounce[k], base + ch.lo, bytes);
+            VCRC_HIP(hipMemcpyAsync(g_ctx.d_slot[k], g_ctx.h_bounce[k], bytes, hipMemcpyHostToDevice, cs), "H2D frames");
+        }
+        VCRC_HIP(hipEventRecord(g_ctx.h2d_done[k], cs), "hipEventRecord");
+        VCRC_HIP(hipStreamWaitEvent(s, g_ctx.h2d_done[k], 0), "hipStreamWaitEvent");
+        FrameParams p{};
+        p.base = g_ctx.d_slot[k] - ch.lo;  // the kernel only touches base + off within the slot
+        p.off = d_off ? d_off + ch.i0 : nullptr;
+        p.len = d_len ? d_len + ch.i0 : nullptr;
+        if (!off) p.base = g_ctx.d_slot[k];  // strided: frame i0 is at the slot start
+        p.stride = stride;
+        p.flen = flen;
+        p.last_len = flen;
+        p.n = ch.i1 - ch.i0;
+        p.seed0 = p.seed_rest = 0xFFFFFFFFu;
+        p.xorout = 0xFFFFFFFFu;
+        p.out_crc = crc ? d_crc + ch.i0 : nullptr;
+        p.out_hdr = hdr ? d_hdr + ch.i0 : nullptr;
+        p.verify = verify ? 1u : 0u;
+        p.out_ok = ok ? d_ok + ch.i0 : nullptr;
+        p.nbad = d_nbad;
+        if ((st = launch_frames(p, hint, s)) != VAL_OK) return st;
+        VCRC_HIP(hipEventRecord(g_ctx.kern_done[k], s), "hipEventRecord");
+    }
     if (crc) VCRC_HIP(hipMemcpyAsync(crc, d_crc, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H crc");
     if (hdr) VCRC_HIP(hipMemcpyAsync(hdr, d_hdr, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H hdr");
     if (ok) VCRC_HIP(hipMemcpyAsync(ok, d_ok, (size_t)n, hipMemcpyDeviceToHost, s), "D2H ok");
@@ -462,6 +589,18 @@ void val_gpu_shutdown(void)
     if (g_ctx.d_small) (void)hipFree(g_ctx.d_small);
     if (g_ctx.d_consts) (void)hipFree(g_ctx.d_consts);
     g_ctx.d_consts = nullptr;
+    if (g_ctx.copy) (void)hipStreamSynchronize(g_ctx.copy);
+    for (int k = 0; k < 2; k++) {
+        if (g_ctx.d_slot[k]) (void)hipFree(g_ctx.d_slot[k]);
+        if (g_ctx.h_bounce[k]) (void)hipHostFree(g_ctx.h_bounce[k]);
+        if (g_ctx.h2d_done[k]) (void)hipEventDestroy(g_ctx.h2d_done[k]);
+        if (g_ctx.kern_done[k]) (void)hipEventDestroy(g_ctx.kern_done[k]);
+        g_ctx.d_slot[k] = g_ctx.h_bounce[k] = nullptr;
+        g_ctx.h2d_done[k] = g_ctx.kern_done[k] = nullptr;
+    }
+    for (int k = 0; k < 2; k++) g_ctx.d_slot_cap[k] = g_ctx.h_bounce_cap[k] = 0;
+    if (g_ctx.copy) (void)hipStreamDestroy(g_ctx.copy);
+    g_ctx.copy = nullptr;
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx.d_stage = g_ctx.d_small = nullptr;
     g_ctx.d_stage_cap = g_ctx.d_small_cap = 0;
@@ -488,6 +627,29 @@ val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes)
     if (lanes != 0 && !valid_lanes(lanes)) return fail(VAL_ERR_INVALID_ARG, "lanes must be 0 or a power of two <= 64");
     g_forced_lanes.store(lanes, std::memory_order_relaxed);
     return VAL_OK;
+}
+
+val_status_t val_gpu_set_host_chunk_bytes(size_t bytes)
+{
+    g_host_chunk.store(bytes, std::memory_order_relaxed);
+    return VAL_OK;
+}
+
+void *val_gpu_host_alloc(size_t bytes)
+{
+    if (bind_thread() != VAL_OK) return nullptr;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        fail(VAL_ERR_NO_MEMORY, "hipHostMalloc", e);
+        return nullptr;
+    }
+    return p;
+}
+
+void val_gpu_host_free(void *p)
+{
+    if (p) (void)hipHostFree(p);
 }
 
 val_status_t val_gpu_set_prefetch(int depth)
