@@ -263,6 +263,30 @@ def main():
         hi = 2 * bytes_per_launch / (time.perf_counter() - t1) / GIB
         print(f"[bench] host-inclusive (pageable H2D + kernel + D2H): {hi:.2f} GiB/s", file=sys.stderr)
 
+    # cfg5 also names the VAL_RESUME_TAIL verify-window CRC:
+    # region windows over the same stream, timed with HIP events, each checked
+    # against the oracle. Reported beside the frames number, never as `value`.
+    windows = None
+    if ragged and rank == 0:
+        windows = []
+        for wlen in (1 << 10, 8 << 10, 8 << 20, 256 << 20):
+            wlen = min(wlen, int(flat.numel()))
+            win = flat[:wlen]
+            st_out = torch.empty(1, dtype=torch.int32, device=dev)
+            reps = 200 if wlen < (1 << 20) else 20
+            vc.region(win, out=st_out)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                vc.region(win, out=st_out)
+            b.record(stream)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) * 1e3 / reps
+            got = (int(st_out.item()) & 0xFFFFFFFF) ^ 0xFFFFFFFF
+            windows.append({"bytes": wlen, "us": round(us, 2), "GiB_s": round(wlen / (us * 1e-6) / GIB, 1),
+                            "crc_ok": got == _oracle.crc32(win.cpu().numpy())})
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not ragged:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -302,6 +326,7 @@ def main():
                 "lanes_per_frame": "per length class (2/4/8/16)" if ragged else vc.lanes_per_frame(len_hint),
                 "parallelism": f"frame-sharded x{world} (no collective)",
                 "parity_sample_ok": parity,
+                **({"verify_windows": windows} if windows is not None else {}),
             },
             "roofline": {
                 "bound": "hbm",

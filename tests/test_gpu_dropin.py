@@ -68,3 +68,19 @@ def test_window_batching_matches_reference(window, mtu):
     assert r["scan_status"] == 0 and r["scanned"] == r["frames"] and r["consumed"] == r["wire_bytes"], r
     assert r["verify_status"] == -6 and r["gpu_bad"] == r["corrupted"] == r["ref_bad"] == r["ref_crc_errors"], r
     assert r["same_verdict"] == r["frames"], r
+
+
+STRESS = os.path.join(ROOT, "oracle", "stress_provider")
+
+
+@pytest.mark.parametrize("seed,lo,hi,n", [(21, 1, 300000, 2000), (22, 2049, 70000, 1500)])
+def test_provider_stress_random_lengths(seed, lo, hi, n):
+    """The scalar hook (host memory) on random lengths and alignments from one
+    reused buffer, against the oracle, in a fresh process. Pins the pinned
+    staging and context scratch arenas: pageable hipMemcpyAsync and per-call
+    hipMallocAsync once gave ~7% wrong CRCs here."""
+    if not os.path.exists(STRESS):
+        pytest.skip("oracle/stress_provider not built")
+    p = subprocess.run([STRESS, str(n), str(seed), str(lo), str(hi)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    assert "bad=0" in p.stdout

@@ -264,6 +264,33 @@ def test_host_pipeline_chunks(vc, pinned, chunk):
         vc.set_host_chunk_bytes(0)
 
 
+def test_concurrent_streams_share_scratch(vc, dev):
+    """Region and ragged calls on four streams at once: the context's scratch
+    arenas serialise them through events, every result bit-exact."""
+    vc.set_geometry()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    regions, frames = [], []
+    for k, st in enumerate(streams):
+        data = _prng.prng_bytes(900 + k, 3_000_000 + 77_777 * k)
+        base, offs, lens = _ragged(950 + k, 300, 0, 70000)
+        regions.append((torch.from_numpy(data).to(dev), data))
+        frames.append((torch.from_numpy(base).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev),
+                       torch.from_numpy(lens.view(np.int32)).to(dev), base, offs, lens))
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(3):
+        for k, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                r = vc.region(regions[k][0], stream=st)
+                c = vc.frames(frames[k][0], off=frames[k][1], length=frames[k][2], stream=st)
+                outs.append((k, r, c))
+    torch.cuda.synchronize()
+    for k, r, c in outs:
+        assert (int(r.item()) & 0xFFFFFFFF) ^ 0xFFFFFFFF == _oracle.crc32(regions[k][1])
+        _, _, _, base, offs, lens = frames[k]
+        assert np.array_equal(_u32(c), _oracle.frames(base, offs, lens))
+
+
 def test_cfg3_full_size_properties(vc, dev):
     """1 M x 16 KiB explicit-offset DATA frames (BASELINE cfg3, 17.2 GB).
     Size-independent checks: trailer write -> verify round trip has zero

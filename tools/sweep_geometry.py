@@ -50,10 +50,17 @@ def main():
         vc.set_geometry()
         vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr)
         ref = crc.clone()
+        rounds = int(os.environ.get("SWEEP_ROUNDS", "1"))  # >1: combos interleaved, median of round medians
+        res = {c: [] for c in combos}
+        for _ in range(rounds):
+            for G, PF in combos:
+                vc.set_geometry(G, PF)
+                med, best = time_it(lambda: vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr))
+                res[(G, PF)].append((med, best, bool(torch.equal(crc, ref))))
         for G, PF in combos:
-            vc.set_geometry(G, PF)
-            med, best = time_it(lambda: vc.frames(flat, stride=stride, flen=flen, n=n, out_crc=crc, out_hdr=hdr))
-            same = bool(torch.equal(crc, ref))
+            med = float(np.median([r[0] for r in res[(G, PF)]]))
+            best = min(r[1] for r in res[(G, PF)])
+            same = all(r[2] for r in res[(G, PF)])
             gbs = n * flen / (med * 1e-3) / 1e9
             print(f"{name} G={G:2d} PF={PF}: median {med:.3f} ms best {best:.3f} ms "
                   f"{gbs:7.1f} GB/s same={same}", flush=True)

@@ -500,30 +500,48 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 
 // ---- region stage 2 -----------------------------------------------------------
 // Fold per-chunk raw states: chunks 0..n-2 are `clen` bytes, chunk n-1 is
-// `last_len`. One workgroup, pairwise GF(2) tree in LDS.
-constexpr int kMaxChunks = 16384;
+// `last_len`. One workgroup, pairwise GF(2) tree in LDS; level j advances the
+// left state by clen * 2^j bytes with 8 lookups in a nibble map the prologue
+// builds from x^(8 clen 2^j) (one gf2_mul per map entry), the final step by
+// last_len bytes.
+constexpr int kMaxChunks = 8192;
+constexpr int kMaxLevels = 13;  // ceil(log2(kMaxChunks - 1))
 struct CombineParams {
     const uint32_t *states;
     uint32_t n;
     uint32_t *out;
-    uint32_t levels;          // ceil(log2(n-1)) levels of "advance clen * 2^j"
-    uint32_t col[15][32];     // level maps
-    uint32_t last_col[32];    // advance last_len bytes
+    uint32_t levels;               // ceil(log2(n-1)) levels of "advance clen * 2^j"
+    uint32_t xlev[kMaxLevels];     // x^(8 clen 2^j) mod P
+    uint32_t xlast;                // x^(8 last_len) mod P
 };
+
+__device__ __forceinline__ uint32_t map_apply_at(const uint32_t *map, uint32_t a)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r ^= map[k * 16 + ((a >> (4 * k)) & 15u)];
+    return r;
+}
 
 __global__ __launch_bounds__(1024) void k_combine(const CombineParams p)
 {
     __shared__ uint32_t v[kMaxChunks];
+    __shared__ uint32_t maps[(kMaxLevels + 1) * 128];  // level maps, then the last_len map
     const uint32_t m = p.n - 1;          // equal-length chunks
     const uint32_t P = 1u << p.levels;   // padded to a power of two, zeros in front
     for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) v[i] = (i >= P - m) ? p.states[i - (P - m)] : 0u;
+    for (uint32_t t = threadIdx.x; t < (p.levels + 1) * 128u; t += blockDim.x) {
+        const uint32_t j = t >> 7, e = t & 127u;
+        const uint32_t x = j < p.levels ? p.xlev[j] : p.xlast;
+        maps[(j < p.levels ? j : (uint32_t)kMaxLevels) * 128u + e] = gf2_mul(x, (e & 15u) << (4u * (e >> 4)));
+    }
     __syncthreads();
     uint32_t width = P;
     for (uint32_t lv = 0; lv < p.levels; lv++) {
         const uint32_t half = width >> 1;
         uint32_t tmp[kMaxChunks / 2 / 1024];
         int cnt = 0;
-        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) tmp[cnt++] = bitmatrix_apply(v[2 * i], p.col[lv]) ^ v[2 * i + 1];
+        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) tmp[cnt++] = map_apply_at(maps + lv * 128u, v[2 * i]) ^ v[2 * i + 1];
         __syncthreads();
         cnt = 0;
         for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) v[i] = tmp[cnt++];
@@ -532,7 +550,7 @@ __global__ __launch_bounds__(1024) void k_combine(const CombineParams p)
     }
     if (threadIdx.x == 0) {
         const uint32_t head = (m > 0) ? v[0] : 0u;
-        *p.out = bitmatrix_apply(head, p.last_col) ^ p.states[p.n - 1];
+        *p.out = map_apply_at(maps + kMaxLevels * 128u, head) ^ p.states[p.n - 1];
     }
 }
 

@@ -25,8 +25,20 @@ namespace vcrc {
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
+// Device scratch owned by the context and shared by calls on any stream: the
+// caller's stream waits for the previous user's last kernel (an event), so
+// concurrent calls serialise on it instead of allocating per call. Callers
+// hold Ctx::mu from acquire through release.
+struct Arena {
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    hipEvent_t last = nullptr;
+};
+
 struct Ctx {
     std::recursive_mutex mu;
+    Arena region_scratch;         // per-chunk states of a region (<= 32 KiB)
+    Arena bin_scratch;            // ragged binning: counts, plan, sorted order
     bool ready = false;
     int device = -1;
     int cus = 0;
@@ -45,6 +57,8 @@ struct Ctx {
     size_t d_slot_cap[2] = {};
     uint8_t *h_bounce[2] = {};
     size_t h_bounce_cap[2] = {};
+    uint8_t *h_out = nullptr;     // pinned landing buffer of the host APIs' D2H results
+    size_t h_out_cap = 0;
 };
 Ctx g_ctx;
 thread_local std::string t_err;
@@ -238,6 +252,38 @@ val_status_t launch_uniform(FrameParams &p, uint32_t G, hipStream_t s)
 
 // Ragged descriptor batch: counting-sort by length on the device, then one
 // grouped launch planned by bytes per length class (no host synchronisation).
+val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out)
+{
+    if (!a.last) VCRC_HIP(hipEventCreateWithFlags(&a.last, hipEventDisableTiming), "hipEventCreate(arena)");
+    if (a.cap < bytes) {
+        VCRC_HIP(hipEventSynchronize(a.last), "hipEventSynchronize(arena)");  // earlier users are done
+        if (a.d) (void)hipFree(a.d);
+        a.d = nullptr;
+        a.cap = 0;
+        const size_t sz = std::max<size_t>(bytes, 1u << 20);
+        hipError_t e = hipMalloc((void **)&a.d, sz);
+        if (e != hipSuccess) return fail(VAL_ERR_NO_MEMORY, "hipMalloc(scratch)", e);
+        a.cap = sz;
+    }
+    VCRC_HIP(hipStreamWaitEvent(s, a.last, 0), "hipStreamWaitEvent(arena)");
+    *out = a.d;
+    return VAL_OK;
+}
+
+val_status_t arena_release(Arena &a, hipStream_t s)
+{
+    VCRC_HIP(hipEventRecord(a.last, s), "hipEventRecord(arena)");
+    return VAL_OK;
+}
+
+void arena_free(Arena &a)
+{
+    if (a.last) (void)hipEventSynchronize(a.last);
+    if (a.d) (void)hipFree(a.d);
+    if (a.last) (void)hipEventDestroy(a.last);
+    a = Arena{};
+}
+
 val_status_t launch_ragged(FrameParams &p, hipStream_t s)
 {
     const uint32_t n = p.n;
@@ -247,8 +293,10 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
     //          ctab[16] u32 | blockoff[nbin][kBuckets] u32 | order[n] u32
     const size_t sz_heads = 8u * 64u, sz_gcount = (size_t)kBuckets * 4u;
     const size_t total = sz_heads + 2 * sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
+    std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
     uint8_t *scratch = nullptr;
-    VCRC_HIP(hipMallocAsync((void **)&scratch, total, s), "hipMallocAsync(bin scratch)");
+    val_status_t st = arena_acquire(g_ctx.bin_scratch, total, s, &scratch);
+    if (st != VAL_OK) return st;
     uint32_t *heads = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *gcount = heads + sz_heads / 4u;
     uint32_t *bstart = gcount + kBuckets;
@@ -272,9 +320,9 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
         else hipLaunchKernelGGL(k_frames_ragged<1>, dim3(blocks), dim3(kBlock), 0, s, p);
         e = hipGetLastError();
     }
-    (void)hipFreeAsync(scratch, s);
+    st = arena_release(g_ctx.bin_scratch, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
-    return VAL_OK;
+    return st;
 }
 
 // typical_len == 0 with descriptors means "lengths unknown or mixed": bin them.
@@ -288,13 +336,15 @@ val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
 // NULL selects the HIP default (null) stream, as in every HIP API.
 hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 
-// Chunking of a long region into "frames" for stage 1.
+// Chunking of a region into "frames" for stage 1: chunks of 2 KiB or more,
+// doubling until there are at most kMaxChunks (8 K) of them. Stage 1 runs
+// them at 32 lanes per chunk, so a large window fills all 4,096 waves (two
+// chunks each: 256 MiB = 8 K chunks of 32 KiB = 16 rounds per lane).
+constexpr uint32_t kRegionLanes = 32;
 void region_geometry(uint64_t len, uint64_t *clen, uint32_t *nchunks)
 {
-    uint64_t c = 4096;
+    uint64_t c = 2048;
     while ((len + c - 1) / c > (uint64_t)kMaxChunks) c <<= 1;
-    // Prefer >= 8192 chunks of work when the region is large enough.
-    while (c < 65536 && (len + 2 * c - 1) / (2 * c) >= 8192) c <<= 1;
     *clen = c;
     *nchunks = (uint32_t)(len ? (len + c - 1) / c : 1);
 }
@@ -316,8 +366,10 @@ val_status_t region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, u
         p.out_crc = d_out;
         return launch_frames(p, (uint32_t)len, s);
     }
+    std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
     uint32_t *d_states = nullptr;
-    VCRC_HIP(hipMallocAsync((void **)&d_states, (size_t)n * 4u, s), "hipMallocAsync(region scratch)");
+    val_status_t st = arena_acquire(g_ctx.region_scratch, (size_t)n * 4u, s, reinterpret_cast<uint8_t **>(&d_states));
+    if (st != VAL_OK) return st;
     FrameParams p{};
     p.base = d_ptr;
     p.stride = clen;
@@ -328,9 +380,10 @@ val_status_t region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, u
     p.seed_rest = 0;
     p.xorout = 0;
     p.out_crc = d_states;
-    val_status_t st = launch_frames(p, (uint32_t)clen, s);
+    fill_constants(p);
+    st = launch_uniform(p, forced_lanes() ? forced_lanes() : kRegionLanes, s);
     if (st != VAL_OK) {
-        (void)hipFreeAsync(d_states, s);
+        (void)arena_release(g_ctx.region_scratch, s);
         return st;
     }
     CombineParams cp{};
@@ -340,13 +393,14 @@ val_status_t region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, u
     uint32_t m = n - 1, levels = 0;
     while ((1u << levels) < m) levels++;
     cp.levels = levels;
-    for (uint32_t j = 0; j < levels; j++) gf2_shift_columns(clen << j, cp.col[j]);
-    gf2_shift_columns(p.last_len, cp.last_col);
+    uint32_t x = gf2_x8n(clen);
+    for (uint32_t j = 0; j < levels; j++, x = gf2_mul(x, x)) cp.xlev[j] = x;
+    cp.xlast = gf2_x8n(p.last_len);
     hipLaunchKernelGGL(k_combine, dim3(1), dim3(1024), 0, s, cp);
     hipError_t e = hipGetLastError();
-    (void)hipFreeAsync(d_states, s);
+    st = arena_release(g_ctx.region_scratch, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "k_combine launch", e);
-    return VAL_OK;
+    return st;
 }
 
 val_status_t grow(uint8_t **buf, size_t *cap, size_t need)
@@ -360,37 +414,6 @@ val_status_t grow(uint8_t **buf, size_t *cap, size_t need)
     if (e != hipSuccess) return fail(VAL_ERR_NO_MEMORY, "hipMalloc(staging)", e);
     *cap = sz;
     return VAL_OK;
-}
-
-// Host pointer -> region state (used by the scalar hooks).
-val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32_t *state_out)
-{
-    val_status_t st = bind_thread();
-    if (st != VAL_OK) return st;
-    std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
-    if ((st = grow(&g_ctx.d_stage, &g_ctx.d_stage_cap, len ? len : 1)) != VAL_OK) return st;
-    if ((st = grow(&g_ctx.d_small, &g_ctx.d_small_cap, 64)) != VAL_OK) return st;
-    hipStream_t s = g_ctx.stream;
-    if (len) VCRC_HIP(hipMemcpyAsync(g_ctx.d_stage, data, len, hipMemcpyHostToDevice, s), "H2D");
-    uint32_t *d_out = reinterpret_cast<uint32_t *>(g_ctx.d_small);
-    if ((st = region_dev(g_ctx.d_stage, len, state_in, d_out, s)) != VAL_OK) return st;
-    VCRC_HIP(hipMemcpyAsync(state_out, d_out, 4, hipMemcpyDeviceToHost, s), "D2H");
-    VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
-    return VAL_OK;
-}
-
-[[noreturn]] void die(const char *fn)
-{
-    fprintf(stderr, "val_crc32_gpu: %s failed on the GPU path: %s (no CPU fallback by design)\n", fn, t_err.c_str());
-    abort();
-}
-
-uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t len)
-{
-    uint32_t out = 0;
-    if (len && !data) die(fn);
-    if (region_host(data, len, state, &out) != VAL_OK) die(fn);
-    return out;
 }
 
 std::atomic<size_t> g_host_chunk{0};
@@ -444,6 +467,62 @@ val_status_t grow_pinned(uint8_t **buf, size_t *cap, size_t need)
     return VAL_OK;
 }
 
+// Pageable host -> device, through the two pinned bounce buffers on stream s.
+// hipMemcpyAsync straight from pageable memory is not used anywhere: on this
+// ROCm it let the next kernel on a non-blocking stream read part of a > 64 KiB
+// copy before it landed (tools/stress/stress_provider.c: ~7% wrong CRCs on
+// 64-70 KiB provider calls, none through pinned staging).
+val_status_t h2d_staged(uint8_t *dst, const uint8_t *src, size_t bytes, hipStream_t s)
+{
+    if (!bytes) return VAL_OK;
+    const size_t chunk = std::min(bytes, host_chunk_bytes());
+    val_status_t st;
+    for (int k = 0; k < 2; k++)
+        if ((st = grow_pinned(&g_ctx.h_bounce[k], &g_ctx.h_bounce_cap[k], chunk)) != VAL_OK) return st;
+    int k = 0;
+    for (size_t o = 0; o < bytes; o += chunk, k ^= 1) {
+        const size_t nb = std::min(chunk, bytes - o);
+        VCRC_HIP(hipEventSynchronize(g_ctx.h2d_done[k]), "hipEventSynchronize");  // bounce k drained
+        parallel_copy(g_ctx.h_bounce[k], src + o, nb);
+        VCRC_HIP(hipMemcpyAsync(dst + o, g_ctx.h_bounce[k], nb, hipMemcpyHostToDevice, s), "H2D");
+        VCRC_HIP(hipEventRecord(g_ctx.h2d_done[k], s), "hipEventRecord");
+    }
+    return VAL_OK;
+}
+
+// Host pointer -> region state (used by the scalar hooks).
+val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32_t *state_out)
+{
+    val_status_t st = bind_thread();
+    if (st != VAL_OK) return st;
+    std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
+    if ((st = grow(&g_ctx.d_stage, &g_ctx.d_stage_cap, len ? len : 1)) != VAL_OK) return st;
+    if ((st = grow(&g_ctx.d_small, &g_ctx.d_small_cap, 64)) != VAL_OK) return st;
+    if ((st = grow_pinned(&g_ctx.h_out, &g_ctx.h_out_cap, 64)) != VAL_OK) return st;
+    hipStream_t s = g_ctx.stream;
+    if ((st = h2d_staged(g_ctx.d_stage, static_cast<const uint8_t *>(data), len, s)) != VAL_OK) return st;
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(g_ctx.d_small);
+    if ((st = region_dev(g_ctx.d_stage, len, state_in, d_out, s)) != VAL_OK) return st;
+    VCRC_HIP(hipMemcpyAsync(g_ctx.h_out, d_out, 4, hipMemcpyDeviceToHost, s), "D2H");
+    VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
+    memcpy(state_out, g_ctx.h_out, 4);
+    return VAL_OK;
+}
+
+[[noreturn]] void die(const char *fn)
+{
+    fprintf(stderr, "val_crc32_gpu: %s failed on the GPU path: %s (no CPU fallback by design)\n", fn, t_err.c_str());
+    abort();
+}
+
+uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t len)
+{
+    uint32_t out = 0;
+    if (len && !data) die(fn);
+    if (region_host(data, len, state, &out) != VAL_OK) die(fn);
+    return out;
+}
+
 // Host-memory batches: descriptors H2D once, then frames in chunks of whole
 // frames (<= host_chunk_bytes of wire span each) through two device slots:
 // chunk c's H2D on the copy stream overlaps chunk c-1's kernel on the compute
@@ -482,8 +561,10 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     uint32_t *d_nbad = d_hdr + n;
     uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_nbad + 4);
     if (off) {
-        VCRC_HIP(hipMemcpyAsync(d_off, off, (size_t)n * 8u, hipMemcpyHostToDevice, s), "H2D off");
-        VCRC_HIP(hipMemcpyAsync(d_len, len, (size_t)n * 4u, hipMemcpyHostToDevice, s), "H2D len");
+        if ((st = h2d_staged(reinterpret_cast<uint8_t *>(d_off), reinterpret_cast<const uint8_t *>(off), (size_t)n * 8u, s)) != VAL_OK)
+            return st;
+        if ((st = h2d_staged(reinterpret_cast<uint8_t *>(d_len), reinterpret_cast<const uint8_t *>(len), (size_t)n * 4u, s)) != VAL_OK)
+            return st;
     }
     VCRC_HIP(hipMemsetAsync(d_nbad, 0, 4, s), "memset");
     // chunks of whole frames [i0, i1) covering wire bytes [lo, hi)
@@ -521,8 +602,6 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     // no slot may be refilled before the previous call's kernels finished with it
     VCRC_HIP(hipEventRecord(g_ctx.kern_done[0], s), "hipEventRecord");
     VCRC_HIP(hipEventRecord(g_ctx.kern_done[1], s), "hipEventRecord");
-    VCRC_HIP(hipEventRecord(g_ctx.h2d_done[0], cs), "hipEventRecord");
-    VCRC_HIP(hipEventRecord(g_ctx.h2d_done[1], cs), "hipEventRecord");
     const uint32_t hint = (off && lmin != lmax) ? 0u : lmax;
     for (size_t c = 0; c < chunks.size(); c++) {
         const Chunk &ch = chunks[c];
@@ -557,12 +636,16 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         if ((st = launch_frames(p, hint, s)) != VAL_OK) return st;
         VCRC_HIP(hipEventRecord(g_ctx.kern_done[k], s), "hipEventRecord");
     }
-    if (crc) VCRC_HIP(hipMemcpyAsync(crc, d_crc, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H crc");
-    if (hdr) VCRC_HIP(hipMemcpyAsync(hdr, d_hdr, (size_t)n * 4u, hipMemcpyDeviceToHost, s), "D2H hdr");
-    if (ok) VCRC_HIP(hipMemcpyAsync(ok, d_ok, (size_t)n, hipMemcpyDeviceToHost, s), "D2H ok");
-    uint32_t bad = 0;
-    VCRC_HIP(hipMemcpyAsync(&bad, d_nbad, 4, hipMemcpyDeviceToHost, s), "D2H nbad");
+    // results land in pinned memory (d_crc | d_hdr | d_nbad | d_ok are contiguous), then are copied out
+    if ((st = grow_pinned(&g_ctx.h_out, &g_ctx.h_out_cap, out_bytes)) != VAL_OK) return st;
+    VCRC_HIP(hipMemcpyAsync(g_ctx.h_out, d_crc, out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
     VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
+    const uint8_t *h = g_ctx.h_out;
+    if (crc) memcpy(crc, h, (size_t)n * 4u);
+    if (hdr) memcpy(hdr, h + (size_t)n * 4u, (size_t)n * 4u);
+    uint32_t bad = 0;
+    memcpy(&bad, h + (size_t)n * 8u, 4);
+    if (ok) memcpy(ok, h + (size_t)n * 8u + 16u, (size_t)n);
     if (nbad) *nbad = bad;
     return VAL_OK;
 }
@@ -594,6 +677,7 @@ void val_gpu_shutdown(void)
         if (g_ctx.d_slot[k]) (void)hipFree(g_ctx.d_slot[k]);
         if (g_ctx.h_bounce[k]) (void)hipHostFree(g_ctx.h_bounce[k]);
         if (g_ctx.h2d_done[k]) (void)hipEventDestroy(g_ctx.h2d_done[k]);
+        g_ctx.h_bounce_cap[k] = 0;
         if (g_ctx.kern_done[k]) (void)hipEventDestroy(g_ctx.kern_done[k]);
         g_ctx.d_slot[k] = g_ctx.h_bounce[k] = nullptr;
         g_ctx.h2d_done[k] = g_ctx.kern_done[k] = nullptr;
@@ -601,6 +685,11 @@ void val_gpu_shutdown(void)
     for (int k = 0; k < 2; k++) g_ctx.d_slot_cap[k] = g_ctx.h_bounce_cap[k] = 0;
     if (g_ctx.copy) (void)hipStreamDestroy(g_ctx.copy);
     g_ctx.copy = nullptr;
+    arena_free(g_ctx.region_scratch);
+    arena_free(g_ctx.bin_scratch);
+    if (g_ctx.h_out) (void)hipHostFree(g_ctx.h_out);
+    g_ctx.h_out = nullptr;
+    g_ctx.h_out_cap = 0;
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx.d_stage = g_ctx.d_small = nullptr;
     g_ctx.d_stage_cap = g_ctx.d_small_cap = 0;
