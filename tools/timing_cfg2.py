@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Per-wave timeline of one frames launch from a -DVCRC_TIMING build
+(tools/build_rev.sh WT build/libval_T.so -DVCRC_TIMING): start, after the LDS
+prologue, end (s_memrealtime, 100 MHz). usage: timing_cfg2.py LIB [workload G]."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import val_protocol_amd.crc as vc  # noqa: E402
+from tools.ab_libs import load, workload  # noqa: E402
+
+vc._lib = load(sys.argv[1])
+vc._lib.vcrc_debug_times.argtypes = [ctypes.c_void_p]
+vc._lib.vcrc_debug_times.restype = ctypes.c_int
+name = sys.argv[2] if len(sys.argv) > 2 else "cfg2"
+G = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+dev = torch.device("cuda:0")
+vc.init(0)
+w, nbytes = workload(name, dev)
+out = torch.empty(w["n"], dtype=torch.int32, device=dev)
+vc.set_geometry(G)
+buf = np.zeros(4096 * 4, np.uint64)
+for rep in range(4):
+    vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
+    torch.cuda.synchronize()
+    assert vc._lib.vcrc_debug_times(buf.ctypes.data) == 0
+t = buf.reshape(4096, 4)[:, :3].astype(np.int64)
+used = t[:, 0] > 0
+t = t[used]
+t0 = t[:, 0].min()
+us = (t - t0) / 100.0  # 100 MHz -> us
+pct = lambda a: " ".join(f"{np.percentile(a, q):6.2f}" for q in (0, 10, 50, 90, 100))
+print(f"{name} G={G or 'auto'} waves={used.sum()}  (percentiles 0/10/50/90/100, us from first wave start)")
+print("  start     ", pct(us[:, 0]))
+print("  prologue  ", pct(us[:, 1]))
+print("  end       ", pct(us[:, 2]))
+print("  prologue dur", pct(us[:, 1] - us[:, 0]), " hash dur", pct(us[:, 2] - us[:, 1]))

@@ -110,8 +110,12 @@ __device__ __forceinline__ void frame_desc(const FrameParams &p, uint64_t f, uin
         off = p.off[f];
         L = p.len[f];
     } else {
+        // select values, not kernel-argument lvalues: `cond ? p.last_len : p.flen`
+        // made hipcc spill both to scratch, and a scratch-using kernel launches
+        // its waves several us slower
+        const uint32_t flen = p.flen, last = p.last_len;
         off = f * p.stride;
-        L = (f + 1 == p.n) ? p.last_len : p.flen;
+        L = (f + 1 == p.n) ? last : flen;
     }
 }
 
@@ -254,11 +258,26 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 }
 
 // Uniform geometry: persistent grid, each wave hashes 64/G frames per step.
+#ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
+__device__ uint64_t g_vcrc_time[4096 * 4];
+#define VCRC_STAMP(k)                                                                                      \
+    do {                                                                                                   \
+        const uint64_t w_ = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;                            \
+        if ((threadIdx.x & 63) == 0 && w_ < 4096) g_vcrc_time[w_ * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define VCRC_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
+
 template <int G, int PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
+    VCRC_STAMP(0);
     build_lds_tables(p.consts);
     __syncthreads();
+    VCRC_STAMP(1);
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
@@ -278,6 +297,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         off = off_n;
         L = L_n;
     }
+    VCRC_STAMP(2);
 }
 
 // ---- ragged path ------------------------------------------------------------

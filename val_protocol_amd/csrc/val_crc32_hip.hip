@@ -707,6 +707,14 @@ int val_gpu_device_count(void)
 
 uint32_t val_gpu_abi_version(void) { return VAL_GPU_ABI_VERSION; }
 
+#ifdef VCRC_TIMING
+// Diagnostic builds only: copy the per-wave stamps of the last k_frames launch.
+int vcrc_debug_times(uint64_t *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vcrc_time), sizeof(g_vcrc_time)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 const char *val_gpu_last_error(void) { return t_err.c_str(); }
 
 uint32_t val_gpu_lanes_per_frame(uint32_t typical_len) { return lanes_per_frame(typical_len); }
