@@ -331,6 +331,14 @@ def test_cfg3_full_size_properties(vc, dev):
     assert np.array_equal(_u32(hdr)[sample], want_h)
     h0 = _u32(hdr)
     assert np.all(h0 == h0[0])  # every header is identical in this stream
+    # The same 17.2 GB through the descriptor paths (u64 offsets past 4 GiB):
+    # uniform (len_hint) and device-binned ragged (len_hint 0) equal strided.
+    d_off = torch.arange(n, device=dev, dtype=torch.int64) * stride
+    d_len = torch.full((n,), flen, dtype=torch.int32, device=dev)
+    for hint in (flen, 0):
+        c2 = vc.frames(flat, off=d_off, length=d_len, len_hint=hint)
+        torch.cuda.synchronize()
+        assert torch.equal(c2, crc), hint
 
 
 def test_no_cpu_fallback_symbols_loaded(vc):

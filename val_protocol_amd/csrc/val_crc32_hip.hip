@@ -150,14 +150,16 @@ uint32_t lanes_per_frame(uint32_t len)
 // G for a uniform batch of n frames of len bytes: the class's G, doubled while
 // the batch would leave more than half of the machine's waves idle (a small
 // window spreads each frame over more lanes, so its serial chain is shorter),
-// up to 16 lanes and at most one 64-B unit per lane per round.
+// up to 16 lanes (64 for a batch of at most 16 frames) and at most one 64-B
+// unit per lane per round.
 uint32_t lanes_for_batch(uint32_t len, uint64_t n)
 {
     uint32_t G = lanes_per_frame(len);
     if (forced_lanes()) return G;
     const uint64_t waves = (uint64_t)g_ctx.cus * kWavesPerBlock;
     const uint64_t units = len ? (len + kUnit - 1) / kUnit : 1u;
-    while (G < 16 && 2u * G <= units && (n + 64 / G - 1) / (64 / G) * 2u <= waves) G *= 2;
+    const uint32_t cap = n <= 16 ? 64u : 16u;  // a lone frame (scalar hooks, small regions) takes a whole wave
+    while (G < cap && 2u * G <= units && (n + 64 / G - 1) / (64 / G) * 2u <= waves) G *= 2;
     return G;
 }
 
@@ -341,8 +343,14 @@ hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 // them at 32 lanes per chunk, so a large window fills all 4,096 waves (two
 // chunks each: 256 MiB = 8 K chunks of 32 KiB = 16 rounds per lane).
 constexpr uint32_t kRegionLanes = 32;
+constexpr uint64_t kRegionOneFrame = 64u << 10;  // up to 64 KiB: one K1 "frame" at 64 lanes, no combine
 void region_geometry(uint64_t len, uint64_t *clen, uint32_t *nchunks)
 {
+    if (len <= kRegionOneFrame) {
+        *clen = len ? len : 1;
+        *nchunks = 1;
+        return;
+    }
     uint64_t c = 2048;
     while ((len + c - 1) / c > (uint64_t)kMaxChunks) c <<= 1;
     *clen = c;
@@ -500,12 +508,24 @@ val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32
     if ((st = grow(&g_ctx.d_small, &g_ctx.d_small_cap, 64)) != VAL_OK) return st;
     if ((st = grow_pinned(&g_ctx.h_out, &g_ctx.h_out_cap, 64)) != VAL_OK) return st;
     hipStream_t s = g_ctx.stream;
-    if ((st = h2d_staged(g_ctx.d_stage, static_cast<const uint8_t *>(data), len, s)) != VAL_OK) return st;
-    uint32_t *d_out = reinterpret_cast<uint32_t *>(g_ctx.d_small);
-    if ((st = region_dev(g_ctx.d_stage, len, state_in, d_out, s)) != VAL_OK) return st;
-    VCRC_HIP(hipMemcpyAsync(g_ctx.h_out, d_out, 4, hipMemcpyDeviceToHost, s), "D2H");
+    // The kernel writes the state straight into pinned host memory (no D2H
+    // command). Inputs up to kZeroCopy are read by the kernel from a pinned
+    // bounce buffer in place (zero-copy over PCIe, no H2D command); longer
+    // ones are staged into HBM first.
+    constexpr size_t kZeroCopy = 16u << 10;
+    const uint8_t *src = g_ctx.d_stage;
+    if (len && len <= kZeroCopy) {
+        if ((st = grow_pinned(&g_ctx.h_bounce[0], &g_ctx.h_bounce_cap[0], len)) != VAL_OK) return st;
+        VCRC_HIP(hipEventSynchronize(g_ctx.h2d_done[0]), "hipEventSynchronize");
+        memcpy(g_ctx.h_bounce[0], data, len);
+        src = g_ctx.h_bounce[0];
+    } else if ((st = h2d_staged(g_ctx.d_stage, static_cast<const uint8_t *>(data), len, s)) != VAL_OK) {
+        return st;
+    }
+    uint32_t *h_state = reinterpret_cast<uint32_t *>(g_ctx.h_out);
+    if ((st = region_dev(src, len, state_in, h_state, s)) != VAL_OK) return st;
     VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
-    memcpy(state_out, g_ctx.h_out, 4);
+    memcpy(state_out, h_state, 4);
     return VAL_OK;
 }
 
