@@ -21,15 +21,18 @@ G = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 dev = torch.device("cuda:0")
 vc.init(0)
 w, nbytes = workload(name, dev)
-out = torch.empty(w["n"], dtype=torch.int32, device=dev)
+out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
 vc.set_geometry(G)
 buf = np.zeros(4096 * 4, np.uint64)
 for rep in range(4):
-    vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
+    if "off" in w:
+        vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=w["len_hint"])
+    else:
+        vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
     torch.cuda.synchronize()
     assert vc._lib.vcrc_debug_times(buf.ctypes.data) == 0
 t = buf.reshape(4096, 4)[:, :3].astype(np.int64)
-used = t[:, 0] > 0
+used = (t[:, 0] > 0) & (t[:, 2] > 0)
 t = t[used]
 t0 = t[:, 0].min()
 us = (t - t0) / 100.0  # 100 MHz -> us
@@ -39,3 +42,12 @@ print("  start     ", pct(us[:, 0]))
 print("  prologue  ", pct(us[:, 1]))
 print("  end       ", pct(us[:, 2]))
 print("  prologue dur", pct(us[:, 1] - us[:, 0]), " hash dur", pct(us[:, 2] - us[:, 1]))
+# where the late waves are: by XCD (block % 8), by wave slot in the block
+blk = np.nonzero(used)[0] // 16
+end = us[:, 2]
+print("  end by blockIdx%8 (median us):", " ".join(f"{np.median(end[blk % 8 == x]):7.1f}" for x in range(8)))
+slot = np.nonzero(used)[0] % 16
+print("  end by wave slot (median us):  ", " ".join(f"{np.median(end[slot == k]):6.0f}" for k in range(16)))
+per_block = np.array([end[blk == b].max() for b in np.unique(blk)])
+print("  per-block max end percentiles:", pct(per_block))
+print("  within-block spread (max-min) median:", np.median([end[blk == b].max() - end[blk == b].min() for b in np.unique(blk)]))

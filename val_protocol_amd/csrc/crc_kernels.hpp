@@ -257,7 +257,6 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     }
 }
 
-// Uniform geometry: persistent grid, each wave hashes 64/G frames per step.
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
 __device__ uint64_t g_vcrc_time[4096 * 4];
 #define VCRC_STAMP(k)                                                                                      \
@@ -271,6 +270,12 @@ __device__ uint64_t g_vcrc_time[4096 * 4];
     } while (0)
 #endif
 
+// Uniform geometry: persistent grid, each wave hashes 64/G frames per step;
+// wave w takes groups w, w + nwaves, ... The four waves of a SIMD finish in
+// age order (cfg3: 2.59 / 2.62 / 2.71 / 2.88 ms, the oldest issues first), but
+// a dynamic work queue that evened them out measured 3-5% slower on cfg3,
+// cfg4 and unaligned uniform batches (profiles/r01_ab_dynamic_uniform.log):
+// the static deal is kept.
 template <int G, int PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
@@ -474,8 +479,10 @@ __device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, 
 template <int PF>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
+    VCRC_STAMP(0);
     build_lds_tables(p.consts);
     __syncthreads();
+    VCRC_STAMP(1);
     const uint32_t *ctab = p.plan;
     const uint32_t items = ctab[12];
     const int lane = threadIdx.x & 63;
@@ -507,7 +514,10 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
         }
         const int G = class_lanes(cur.c);
         hash_frame<0, PF>(p, f, active, off, L, lane & (G - 1), sb, G);
-        if (it_n >= items) break;
+        if (it_n >= items) {
+            VCRC_STAMP(2);
+            break;
+        }
         it = it_n;
         it_n = part + P * (__builtin_amdgcn_readfirstlane(k_nn) + 2u * nwp);
         cur = nxt;
