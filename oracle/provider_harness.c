@@ -24,6 +24,11 @@
  *       stream, with some frames corrupted, goes through the reference RX
  *       (val_internal_recv_packet per frame) and through val_frame_scan +
  *       one val_crc32_verify_frames_host launch: same verdict per frame.
+ *   provider_harness <libval_crc_hip.so> windowbench <W> <mtu> <reps>
+ *       f1/f2 measured: one window of W DATA frames framed + CRC'd + sent by
+ *       the reference TX one frame at a time vs the batched GPU path, and
+ *       received + verified by the reference RX vs scan + one GPU verify
+ *       (see mode_windowbench).
  *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
  *       full val_send_files / val_receive_files transfer over an in-memory
  *       duplex pipe (the reference test strategy), provider on
@@ -362,6 +367,166 @@ static int mode_window(uint32_t W, size_t mtu)
     return 0;
 }
 
+/* ---- windowbench: call-site batching measured end to end
+ * Linear in-memory transport (memcpy; no digest), so the timed work is the
+ * framing + CRC + transport copy of one window of W DATA frames:
+ *   ref_tx   reference TX, one val_internal_send_packet_ex per frame (CPU CRC)
+ *   gpu_tx   val_frame_data_batch into a pinned window buffer + one
+ *            val_crc32_frames_host launch + val_frame_put_trailers + one
+ *            transport send per frame
+ *   ref_rx   reference RX, one val_internal_recv_packet per frame (CPU CRC)
+ *   gpu_rx   the window's bytes read in one transport call into a pinned
+ *            ring + val_frame_scan + one val_crc32_verify_frames_host launch
+ * Median of REPS windows each; parity: byte-identical TX streams, every frame
+ * accepted on both RX paths. */
+typedef struct {
+    uint8_t *buf;
+    size_t cap, wpos, rpos;
+} sink_t;
+
+static int sink_send(void *ctx, const void *data, size_t len)
+{
+    sink_t *k = (sink_t *)ctx;
+    if (k->wpos + len > k->cap) return -1;
+    memcpy(k->buf + k->wpos, data, len);
+    k->wpos += len;
+    return (int)len;
+}
+
+static int sink_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
+{
+    (void)timeout_ms;
+    sink_t *k = (sink_t *)ctx;
+    const size_t n = size <= k->wpos - k->rpos ? size : k->wpos - k->rpos;
+    memcpy(buffer, k->buf + k->rpos, n);
+    k->rpos += n;
+    if (got) *got = n;
+    return 0;
+}
+
+static double now_us(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec / 1e3;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+    const double x = *(const double *)a, y = *(const double *)b;
+    return (x > y) - (x < y);
+}
+
+static double median(double *v, int n)
+{
+    qsort(v, (size_t)n, sizeof(double), cmp_d);
+    return v[n / 2];
+}
+
+typedef void *(*fn_alloc_t)(size_t);
+
+static int mode_windowbench(uint32_t W, size_t mtu, int reps)
+{
+    fn_batch_t batch = (fn_batch_t)dlsym(g_lib, "val_frame_data_batch");
+    fn_frames_host_t frames = (fn_frames_host_t)dlsym(g_lib, "val_crc32_frames_host");
+    fn_put_t put = (fn_put_t)dlsym(g_lib, "val_frame_put_trailers");
+    fn_scan_t scan = (fn_scan_t)dlsym(g_lib, "val_frame_scan");
+    fn_verify_t verify = (fn_verify_t)dlsym(g_lib, "val_crc32_verify_frames_host");
+    fn_alloc_t halloc = (fn_alloc_t)dlsym(g_lib, "val_gpu_host_alloc");
+    if (!batch || !frames || !put || !scan || !verify || !halloc) return 2;
+    const size_t maxp = mtu - 12;
+    const uint64_t file_size = (uint64_t)W * (maxp - 8);
+    uint8_t *file = (uint8_t *)malloc(file_size);
+    oracle_prng_fill(0x5151, file, file_size);
+    uint64_t *pay_off = calloc(W, 8), *file_off = calloc(W, 8), *fo = calloc(W, 8), *fo2 = calloc(W, 8);
+    uint32_t *pay_len = calloc(W, 4), *cl = calloc(W, 4), *cl2 = calloc(W, 4), *crc = calloc(W, 4);
+    uint8_t *inc = calloc(W, 1), *ok = calloc(W, 1);
+    uint32_t nf = 0;
+    for (uint64_t pos = 0; pos < file_size && nf < W; nf++) {
+        inc[nf] = (nf == 0); /* explicit offset on the window's first frame (src/val_sender.c:833) */
+        size_t take = maxp - (inc[nf] ? 8u : 0u);
+        if (take > file_size - pos) take = (size_t)(file_size - pos);
+        pay_off[nf] = file_off[nf] = pos;
+        pay_len[nf] = (uint32_t)take;
+        pos += take;
+    }
+    const size_t cap = (size_t)W * mtu + 4096;
+    sink_t ks = {(uint8_t *)malloc(cap), cap, 0, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, NULL, mtu, NULL);
+    cfg.transport.send = sink_send;
+    cfg.transport.recv = sink_recv;
+    cfg.transport.io_context = &ks;
+    val_session_t *s = NULL;
+    if (val_session_create(&cfg, &s, NULL) != VAL_OK) return 3;
+    double *t = (double *)malloc(sizeof(double) * (size_t)reps);
+    /* reference TX */
+    for (int r = 0; r < reps; r++) {
+        ks.wpos = 0;
+        const double t0 = now_us();
+        for (uint32_t i = 0; i < nf; i++)
+            if (val_internal_send_packet_ex(s, VAL_PKT_DATA, file + pay_off[i], pay_len[i], file_off[i], inc[i]) != VAL_OK) return 4;
+        t[r] = now_us() - t0;
+    }
+    const double ref_tx = median(t, reps);
+    const size_t wire = ks.wpos;
+    uint8_t *ref = (uint8_t *)malloc(wire);
+    memcpy(ref, ks.buf, wire);
+    /* batched GPU TX */
+    uint8_t *stage = (uint8_t *)halloc((size_t)W * mtu);
+    if (!stage) return 5;
+    size_t used = 0;
+    for (int r = 0; r < reps; r++) {
+        ks.wpos = 0;
+        const double t0 = now_us();
+        if (batch(file, pay_off, pay_len, file_off, inc, nf, stage, (size_t)W * mtu, fo, cl, &used) != 0) return 6;
+        if (frames(stage, used, fo, cl, 0, 0, nf, crc, NULL) != 0) return 7;
+        put(stage, fo, cl, crc, nf);
+        for (uint32_t i = 0; i < nf; i++) sink_send(&ks, stage + fo[i], cl[i] + 4u);
+        t[r] = now_us() - t0;
+    }
+    const double gpu_tx = median(t, reps);
+    const int tx_equal = ks.wpos == wire && memcmp(ks.buf, ref, wire) == 0;
+    /* reference RX */
+    uint8_t *out = (uint8_t *)malloc(mtu);
+    uint32_t ref_ok = 0;
+    for (int r = 0; r < reps; r++) {
+        ks.rpos = 0;
+        uint32_t good = 0;
+        const double t0 = now_us();
+        for (uint32_t i = 0; i < nf; i++) {
+            val_packet_type_t ty = 0;
+            uint32_t plen = 0;
+            uint64_t off = 0;
+            good += val_internal_recv_packet(s, &ty, out, (uint32_t)mtu, &plen, &off, 100) == VAL_OK;
+        }
+        t[r] = now_us() - t0;
+        ref_ok = good;
+    }
+    const double ref_rx = median(t, reps);
+    /* batched GPU RX */
+    uint8_t *ring = (uint8_t *)halloc(wire);
+    if (!ring) return 8;
+    uint32_t nscan = 0, nbad = 0;
+    int vst = 0;
+    for (int r = 0; r < reps; r++) {
+        ks.rpos = 0;
+        const double t0 = now_us();
+        size_t got = 0, consumed = 0;
+        sink_recv(&ks, ring, wire, &got, 0);
+        if (scan(ring, got, mtu, nf, fo2, cl2, &nscan, &consumed) != 0) return 9;
+        vst = verify(ring, got, fo2, cl2, 0, 0, nscan, ok, &nbad);
+        t[r] = now_us() - t0;
+    }
+    const double gpu_rx = median(t, reps);
+    printf("{\"mode\":\"windowbench\",\"frames\":%u,\"mtu\":%zu,\"wire_bytes\":%zu,\"reps\":%d,"
+           "\"ref_tx_us\":%.1f,\"gpu_tx_us\":%.1f,\"ref_rx_us\":%.1f,\"gpu_rx_us\":%.1f,"
+           "\"tx_equal\":%d,\"ref_rx_ok\":%u,\"gpu_rx_scanned\":%u,\"gpu_rx_status\":%d,\"gpu_rx_bad\":%u}\n",
+           nf, mtu, wire, reps, ref_tx, gpu_tx, ref_rx, gpu_rx, tx_equal, ref_ok, nscan, vst, nbad);
+    val_session_destroy(s);
+    return 0;
+}
+
 typedef struct {
     val_session_t *rx;
     const char *dir;
@@ -464,6 +629,10 @@ int main(int argc, char **argv)
     if (!strcmp(argv[2], "rx")) return use_gpu ? mode_rx() : 1;
     if (!strcmp(argv[2], "window") && argc >= 5)
         return use_gpu ? mode_window((uint32_t)strtoul(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0)) : 1;
+    if (!strcmp(argv[2], "windowbench") && argc >= 6)
+        return use_gpu ? mode_windowbench((uint32_t)strtoul(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0),
+                                          atoi(argv[5]))
+                       : 1;
     if (!strcmp(argv[2], "loopback") && argc >= 5)
         return mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu);
     fprintf(stderr, "bad mode\n");

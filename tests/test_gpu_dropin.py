@@ -84,3 +84,14 @@ def test_provider_stress_random_lengths(seed, lo, hi, n):
     p = subprocess.run([STRESS, str(n), str(seed), str(lo), str(hi)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     assert "bad=0" in p.stdout
+
+
+@pytest.mark.parametrize("W,mtu", [(64, 1024), (16, 65536)])
+def test_windowbench_batched_call_sites_match_reference(W, mtu):
+    """SURVEY 8(f) f1/f2 end to end: a window framed + CRC'd by the reference TX
+    one frame at a time equals the batched GPU window byte for byte, and the
+    batched scan + GPU verify accepts every frame the reference RX accepts."""
+    r = _run(LIB, "windowbench", str(W), str(mtu), "3")[0]
+    assert r["tx_equal"] == 1, r
+    assert r["ref_rx_ok"] == r["frames"] == r["gpu_rx_scanned"], r
+    assert r["gpu_rx_status"] == 0 and r["gpu_rx_bad"] == 0, r
