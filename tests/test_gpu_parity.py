@@ -221,6 +221,44 @@ def test_host_batch_api(vc):
 
 
 @pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("n,lo,hi", [(1, 0, 3), (16, 1000, 1100), (40, 0, 6000), (3, 60000, 65547)])
+def test_host_small_window_zero_copy(vc, pinned, n, lo, hi):
+    """Windows up to 256 KiB take the one-launch zero-copy host path: strided,
+    packed descriptors (with a non-zero first offset), shuffled descriptors,
+    header_crc, and verify with a corrupted frame."""
+    vc.set_geometry()
+    base, offs, lens = _ragged(77 + n, n, lo, hi)
+    pad = 37  # first frame not at the buffer start
+    base = np.concatenate([np.full(pad, 0xEE, np.uint8), base])
+    offs = offs + np.uint64(pad)
+
+    def host(a):
+        if not pinned:
+            return a
+        pb = vc.PinnedBuffer(a.size)
+        pb.array[:] = a
+        keep.append(pb)
+        return pb.array
+
+    keep = []
+    want, want_h = _oracle.frames(base, offs, lens, header=True)
+    crc, hdr = vc.frames_host(host(base), offs, lens, header=True)
+    assert np.array_equal(crc, want) and np.array_equal(hdr, want_h)
+    perm = np.random.default_rng(n).permutation(n)
+    assert np.array_equal(vc.frames_host(host(base), offs[perm], lens[perm]), want[perm])
+    tr = _with_trailers(base.copy(), offs, lens)
+    st, ok, nbad = vc.verify_frames_host(host(tr), offs, lens)
+    assert st == vc.VAL_OK and nbad == 0 and ok.all()
+    k = n // 2
+    tr[int(offs[k]) + int(lens[k]) + 1] ^= 0x08  # trailer byte
+    st, ok, nbad = vc.verify_frames_host(host(tr), offs, lens)
+    assert st == vc.VAL_ERR_CRC and nbad == 1 and ok[k] == 0
+    stream = _prng.frames_stream(n, 1024, stride_pad=0, seed=0x99)
+    assert np.array_equal(vc.frames_host(host(stream), stride=1044, flen=1040, n=n),
+                          _oracle.frames_strided(stream, 1044, 1040, n))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("chunk", [0, 1 << 16, 200_003])
 def test_host_pipeline_chunks(vc, pinned, chunk):
     """Host-memory batches through the chunked H2D pipeline: strided,
@@ -348,6 +386,12 @@ def test_no_cpu_fallback_symbols_loaded(vc):
 
 
 # ---- ragged path: device binning by length class + grouped launch ------------
+@pytest.fixture
+def binned_always(monkeypatch):
+    """Pin the device-binned path even for batches below its size threshold."""
+    monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+
+
 def _run_ragged(vc, dev, base, offs, lens, header=False):
     vc.set_geometry()  # automatic geometry: len_hint == 0 selects the binned path
     d = torch.from_numpy(base).to(dev)
@@ -361,7 +405,10 @@ def _run_ragged(vc, dev, base, offs, lens, header=False):
 
 @pytest.mark.parametrize("seed,n,lo,hi", [(1, 1, 5, 5), (2, 3, 0, 2000), (3, 700, 0, 70000), (4, 5000, 8, 1023),
                                           (5, 4000, 50000, 66000), (6, 20000, 0, 70000)])
-def test_ragged_binned(vc, dev, seed, n, lo, hi):
+@pytest.mark.parametrize("binned", [True, False])
+def test_ragged_binned(vc, dev, seed, n, lo, hi, binned, monkeypatch):
+    if binned:
+        monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
     base, offs, lens = _ragged(seed, n, lo, hi)
     got, got_h = _run_ragged(vc, dev, base, offs, lens, header=True)
     want, want_h = _oracle.frames(base, offs, lens, header=True)
@@ -369,7 +416,7 @@ def test_ragged_binned(vc, dev, seed, n, lo, hi):
     assert np.array_equal(got_h, want_h)
 
 
-def test_ragged_log_uniform_cfg5_shape(vc, dev):
+def test_ragged_log_uniform_cfg5_shape(vc, dev, binned_always):
     rng = np.random.default_rng(55)
     n = 3000
     lens = (np.exp(rng.uniform(np.log(520), np.log(65532), n))).astype(np.uint32)
@@ -379,7 +426,10 @@ def test_ragged_log_uniform_cfg5_shape(vc, dev):
     assert np.array_equal(got, _oracle.frames(base, offs, lens))
 
 
-def test_ragged_every_length_and_verify(vc, dev):
+@pytest.mark.parametrize("binned", [True, False])
+def test_ragged_every_length_and_verify(vc, dev, binned, monkeypatch):
+    if binned:
+        monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
     lens = np.arange(0, 2500, dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 4)]).astype(np.uint64)
     base = _prng.prng_bytes(57, int(offs[-1]) + 2600)

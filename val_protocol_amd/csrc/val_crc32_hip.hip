@@ -327,11 +327,20 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
     return st;
 }
 
-// typical_len == 0 with descriptors means "lengths unknown or mixed": bin them.
+// typical_len == 0 with descriptors means "lengths unknown or mixed": bin them,
+// unless the batch is too small to fill the machine once (binning is four
+// launches; a small window runs uniform at 16 lanes per frame instead).
+// VAL_GPU_RAGGED_MIN_FRAMES overrides the threshold (tests pin the binned path on small batches).
+uint32_t ragged_min_frames()
+{
+    const char *e = getenv("VAL_GPU_RAGGED_MIN_FRAMES");
+    return e ? (uint32_t)atoi(e) : 4096u;
+}
+
 val_status_t launch_frames(FrameParams &p, uint32_t typical_len, hipStream_t s)
 {
     if (p.n == 0) return VAL_OK;
-    if (p.off && typical_len == 0 && !forced_lanes()) return launch_ragged(p, s);
+    if (p.off && typical_len == 0 && !forced_lanes() && p.n >= ragged_min_frames()) return launch_ragged(p, s);
     return launch_uniform(p, lanes_for_batch(typical_len ? typical_len : 16384u, p.n), s);
 }
 
@@ -543,6 +552,73 @@ uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t l
     return out;
 }
 
+// Small host windows (<= 256 KiB of wire span): one launch and no copy
+// commands. Frames and descriptors sit in one pinned buffer (the caller's, if
+// its frames are pinned already) that the kernel reads in place over PCIe,
+// and the results are written straight into pinned host memory; the mismatch
+// count is taken from the ok flags on the host. A 16-frame 1 KiB window cost
+// ~64 us through the chunked pipeline (a descriptor copy, a memset, a frames
+// copy, a launch, a results copy).
+constexpr uint64_t kHostZeroCopy = 256u << 10;
+val_status_t frames_host_small(const uint8_t *base, uint64_t lo, uint64_t hi, const uint64_t *off, const uint32_t *len,
+                               uint64_t stride, uint32_t flen, uint32_t n, int verify, uint32_t hint, uint32_t *crc,
+                               uint32_t *hdr, uint8_t *ok, uint32_t *nbad)
+{
+    const size_t span = (size_t)(hi - lo), desc = off ? (size_t)n * 12u : 0u;
+    const size_t span_al = (span + 15u) & ~(size_t)15u;
+    const bool pinned = is_pinned(base);
+    val_status_t st;
+    if ((st = grow_pinned(&g_ctx.h_bounce[0], &g_ctx.h_bounce_cap[0], (pinned ? 0u : span_al) + desc + 16u)) != VAL_OK)
+        return st;
+    if ((st = grow_pinned(&g_ctx.h_out, &g_ctx.h_out_cap, (size_t)n * 9u + 16u)) != VAL_OK) return st;
+    VCRC_HIP(hipEventSynchronize(g_ctx.h2d_done[0]), "hipEventSynchronize");  // nothing still reads bounce 0
+    uint8_t *b = g_ctx.h_bounce[0];
+    const uint8_t *frames = base + lo;
+    if (!pinned) {
+        memcpy(b, base + lo, span);
+        frames = b;
+    }
+    uint64_t *h_off = nullptr;
+    uint32_t *h_len = nullptr;
+    if (off) {  // rebased: frame i sits at frames + h_off[i]
+        h_off = reinterpret_cast<uint64_t *>(b + (pinned ? 0u : span_al));
+        h_len = reinterpret_cast<uint32_t *>(h_off + n);
+        for (uint32_t i = 0; i < n; i++) h_off[i] = off[i] - lo;
+        memcpy(h_len, len, (size_t)n * 4u);
+    }
+    uint32_t *h_crc = reinterpret_cast<uint32_t *>(g_ctx.h_out);
+    uint32_t *h_hdr = h_crc + n;
+    uint8_t *h_ok = reinterpret_cast<uint8_t *>(h_hdr + n + 4);
+    FrameParams p{};
+    p.base = frames;
+    p.off = h_off;
+    p.len = h_len;
+    p.stride = stride;
+    p.flen = flen;
+    p.last_len = flen;
+    p.n = n;
+    p.seed0 = p.seed_rest = 0xFFFFFFFFu;
+    p.xorout = 0xFFFFFFFFu;
+    p.out_crc = crc ? h_crc : nullptr;
+    p.out_hdr = hdr ? h_hdr : nullptr;
+    p.verify = verify ? 1u : 0u;
+    p.out_ok = (ok || nbad) ? h_ok : nullptr;
+    p.nbad = nullptr;
+    hipStream_t s = g_ctx.stream;
+    if ((st = launch_frames(p, hint, s)) != VAL_OK) return st;
+    VCRC_HIP(hipEventRecord(g_ctx.h2d_done[0], s), "hipEventRecord");  // the kernel reads bounce 0
+    VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (crc) memcpy(crc, h_crc, (size_t)n * 4u);
+    if (hdr) memcpy(hdr, h_hdr, (size_t)n * 4u);
+    if (ok) memcpy(ok, h_ok, n);
+    if (nbad) {
+        uint32_t bad = 0;
+        for (uint32_t i = 0; i < n; i++) bad += h_ok[i] == 0;
+        *nbad = verify ? bad : 0u;
+    }
+    return VAL_OK;
+}
+
 // Host-memory batches: descriptors H2D once, then frames in chunks of whole
 // frames (<= host_chunk_bytes of wire span each) through two device slots:
 // chunk c's H2D on the copy stream overlaps chunk c-1's kernel on the compute
@@ -571,6 +647,17 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
     const size_t desc_bytes = off ? (size_t)n * 12u : 0u;
     const size_t out_bytes = (size_t)n * 9u + 16u;
+    if (n) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t o = off ? off[i] : (uint64_t)i * stride;
+            lo = std::min(lo, o);
+            hi = std::max(hi, o + (len ? len[i] : flen) + tail);
+        }
+        if (hi - lo <= kHostZeroCopy)
+            return frames_host_small(base, lo, hi, off, len, stride, flen, n, verify, lmin == lmax ? lmax : 0u, crc, hdr, ok,
+                                     nbad);
+    }
     if ((st = grow(&g_ctx.d_small, &g_ctx.d_small_cap, desc_bytes + out_bytes + 64)) != VAL_OK) return st;
     hipStream_t s = g_ctx.stream, cs = g_ctx.copy;
     uint8_t *sm = g_ctx.d_small;
@@ -580,7 +667,15 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     uint32_t *d_hdr = d_crc + n;
     uint32_t *d_nbad = d_hdr + n;
     uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_nbad + 4);
-    if (off) {
+    if (off && (size_t)n * 12u <= host_chunk_bytes()) {
+        // both descriptor arrays through one bounce and one H2D (d_len follows d_off)
+        if ((st = grow_pinned(&g_ctx.h_bounce[0], &g_ctx.h_bounce_cap[0], (size_t)n * 12u)) != VAL_OK) return st;
+        VCRC_HIP(hipEventSynchronize(g_ctx.h2d_done[0]), "hipEventSynchronize");
+        memcpy(g_ctx.h_bounce[0], off, (size_t)n * 8u);
+        memcpy(g_ctx.h_bounce[0] + (size_t)n * 8u, len, (size_t)n * 4u);
+        VCRC_HIP(hipMemcpyAsync(d_off, g_ctx.h_bounce[0], (size_t)n * 12u, hipMemcpyHostToDevice, s), "H2D descriptors");
+        VCRC_HIP(hipEventRecord(g_ctx.h2d_done[0], s), "hipEventRecord");
+    } else if (off) {
         if ((st = h2d_staged(reinterpret_cast<uint8_t *>(d_off), reinterpret_cast<const uint8_t *>(off), (size_t)n * 8u, s)) != VAL_OK)
             return st;
         if ((st = h2d_staged(reinterpret_cast<uint8_t *>(d_len), reinterpret_cast<const uint8_t *>(len), (size_t)n * 4u, s)) != VAL_OK)
