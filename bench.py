@@ -172,6 +172,15 @@ def main():
 
     vc.init(gpu)
     n, payload, explicit, header = CONFIGS[args.config]
+    # cfg4 is one 8 GiB file sharded across the ranks (BASELINE configs[3]):
+    # contiguous frame ranges, no collective on the data path -> strong
+    # scaling. The other configs give every rank its own batch -> weak.
+    strong = args.config == "cfg4"
+    n_total, first = n, rank * n
+    if strong:
+        from val_protocol_amd.shard import shard_frames
+
+        first, n = shard_frames(n_total, world, rank)
     ragged = args.config == "cfg5"
     d_off = d_len = None
     if ragged:
@@ -183,7 +192,7 @@ def main():
         flat = buf
         len_hint = 0  # mixed lengths: the library bins frames by length class on the device
     else:
-        buf, flen, stride = make_frames(torch, dev, n, payload, explicit, rank * n, seed=1234 + rank)
+        buf, flen, stride = make_frames(torch, dev, n, payload, explicit, first, seed=1234 + rank)
         flat = buf.view(-1)
         len_hint = flen
     crc = torch.empty(n, dtype=torch.int32, device=dev)
@@ -250,7 +259,7 @@ def main():
 
     # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
     bytes_per_launch = int(d_len.long().sum().item()) if ragged else n * flen
-    total_bytes = bytes_per_launch * args.steps * world
+    total_bytes = (n_total * flen if strong else bytes_per_launch * world) * args.steps
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
@@ -310,21 +319,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (device-generated random payloads, reference DATA framing)",
             "config": {
-                "workload": (f"{args.config}: {n} DATA frames x "
+                "workload": (f"{args.config}: {n_total if strong else n} DATA frames x "
                              + (f"{CFG5_MIN}-{CFG5_MAX} B log-uniform payload (1 in 8 implied offset), packed unaligned"
-                                if ragged else f"{payload} B payload") + " per GPU, "
-                             f"{'header_crc + ' if header else ''}trailer CRC-32"
+                                if ragged else f"{payload} B payload")
+                             + (f" (one file, sharded over {world} GPU{'s' if world > 1 else ''}), " if strong else " per GPU, ")
+                             + f"{'header_crc + ' if header else ''}trailer CRC-32"
                              f"{' (RX verify)' if args.verify else ''}"),
                 "frames_per_gpu": n,
+                **({"frames_total": n_total} if strong else {}),
                 "crc_input_bytes_per_frame": (bytes_per_launch / n) if ragged else flen,
                 "frame_stride": stride if not ragged else "packed",
                 "lanes_per_frame": "per length class (2/4/8/16)" if ragged else vc.lanes_per_frame(len_hint),
-                "parallelism": f"frame-sharded x{world} (no collective)",
+                "parallelism": (f"one {n_total}-frame file sharded x{world} by contiguous frame ranges (no collective)"
+                                if strong else f"frame-sharded x{world} (no collective)"),
                 "parity_sample_ok": parity,
                 **({"verify_windows": windows} if windows is not None else {}),
             },
