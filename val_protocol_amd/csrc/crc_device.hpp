@@ -88,15 +88,6 @@ __device__ __forceinline__ uint32_t map_apply(uint32_t a, uint32_t map)
 __host__ __device__ constexpr uint32_t gap_map(int gi) { return kLdsMaps + (uint32_t)gi * 512u; }
 __host__ __device__ constexpr uint32_t tree_map(int j) { return kLdsMaps + (7u + (uint32_t)j) * 512u; }
 
-// r = M v for a 32x32 GF(2) matrix given by its columns (wave-uniform, SGPRs).
-__device__ __forceinline__ uint32_t bitmatrix_apply(uint32_t v, const uint32_t *col)
-{
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < 32; i++) r ^= (0u - ((v >> i) & 1u)) & col[i];
-    return r;
-}
-
 // Device constant blob (u32 words, built once per device at init from
 // gf2_crc32.h and kept in HBM; every launch's prologue copies it into LDS, an
 // L2 hit after the first workgroup):

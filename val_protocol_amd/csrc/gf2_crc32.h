@@ -45,11 +45,4 @@ GF2_FN uint32_t gf2_x8n(uint64_t n)
     return result;
 }
 
-/* Columns of the 32x32 bit matrix of r -> r * x^(8n): col[i] = image of bit i. */
-GF2_FN void gf2_shift_columns(uint64_t nbytes, uint32_t col[32])
-{
-    uint32_t x = gf2_x8n(nbytes);
-    for (int i = 0; i < 32; i++) col[i] = gf2_mul(x, 1u << i);
-}
-
 #endif /* VAL_GF2_CRC32_H */
