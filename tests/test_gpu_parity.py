@@ -302,15 +302,19 @@ def test_host_pipeline_chunks(vc, pinned, chunk):
         vc.set_host_chunk_bytes(0)
 
 
-def test_concurrent_streams_share_scratch(vc, dev):
+def test_concurrent_streams_share_scratch(vc, dev, monkeypatch):
     """Region and ragged calls on four streams at once: the context's scratch
-    arenas serialise them through events, every result bit-exact."""
+    arenas serialise them through events, every result bit-exact. The frame
+    batches take the device-binned path (its bucket totals are re-zeroed by
+    each batch's last kernel for the next one) and differ in size, so the bin
+    scratch also grows between calls."""
+    monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
     vc.set_geometry()
     streams = [torch.cuda.Stream() for _ in range(4)]
     regions, frames = [], []
     for k, st in enumerate(streams):
         data = _prng.prng_bytes(900 + k, 3_000_000 + 77_777 * k)
-        base, offs, lens = _ragged(950 + k, 300, 0, 70000)
+        base, offs, lens = _ragged(950 + k, 300 + 1200 * k, 0, 70000)
         regions.append((torch.from_numpy(data).to(dev), data))
         frames.append((torch.from_numpy(base).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev),
                        torch.from_numpy(lens.view(np.int32)).to(dev), base, offs, lens))

@@ -41,18 +41,23 @@ def workload(name, dev):
         lens = rng.integers(520, 65533, 262144)
     elif name == "u57":
         lens = np.full(56508, 57000)
-    elif name in ("c2", "c2a"):  # class-2 log-uniform mix; c2a: lengths = 12 mod 16 (16-B aligned frame starts)
+    elif name in ("c2", "c2a", "c2b", "c2d"):  # class-2 log-uniform mix, variants by alignment:
+        # c2a: L = 12 mod 16 (frame starts 16-B aligned, units 12 mod 16, no tail bytes);
+        # c2b: L = 0 mod 4 (no tail bytes, units at random 16-B phase);
+        # c2d: as c2a with the stream shifted by 4 B (units 16-B aligned, no tail bytes)
         lens = np.exp(rng.uniform(np.log(8192), np.log(49151), 150000)).astype(np.int64)
-        if name == "c2a":
+        if name in ("c2a", "c2d"):
             lens = (lens // 16) * 16 + 12
+        elif name == "c2b":
+            lens = (lens // 4) * 4
     elif name.startswith("u") and name.rstrip("d")[1:].isdigit():  # uNNNN: uniform length NNNN, ragged path;
         L = int(name.rstrip("d")[1:])                              # uNNNNd: same, descriptor-uniform (len_hint)
         lens = np.full(max(1, (3 << 30) // (L + 4)), L)
     else:
         raise SystemExit(name)
     wire = lens + 4
-    off = np.concatenate([[0], np.cumsum(wire)[:-1]])
-    buf = torch.randint(0, 256, (int(wire.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    off = np.concatenate([[0], np.cumsum(wire)[:-1]]) + (4 if name == "c2d" else 0)
+    buf = torch.randint(0, 256, (int(wire.sum()) + 4,), dtype=torch.uint8, device=dev, generator=g)
     return dict(buf=buf, off=torch.from_numpy(off.astype(np.int64)).to(dev),
                 length=torch.from_numpy(lens.astype(np.int32)).to(dev),
                 len_hint=int(lens[0]) if name.endswith("d") else 0), int(lens.sum())

@@ -53,6 +53,7 @@ struct FrameParams {
     const uint32_t *order;   // grouped mode: class-sorted frame indices
     const uint32_t *plan;    // ragged mode: class table {cstart[4], ccount[4], istart[5]}
     uint32_t *heads;         // ragged mode: 8 work-queue heads, 64 B apart, zero on entry
+    uint32_t *bin_counts;    // ragged mode: k_bin_count's bucket totals, re-zeroed here for the next batch
     const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
 };
 
@@ -347,40 +348,57 @@ __device__ __forceinline__ uint32_t bucket_slot(uint32_t *cnt, int b, bool v)
     return v ? atomicAdd(&cnt[b], 1u) : 0u;
 }
 
+// Lengths of a binning workgroup's slice are read kBinBatch per thread before
+// any is used: one memory latency per batch instead of one per 256 frames
+// (a dependent load -> atomic loop made each binning pass ~8 us).
+constexpr int kBinThreads = 256, kBinBatch = 8;
+
+template <typename F>
+__device__ __forceinline__ void for_each_bucket(const uint32_t *len, uint64_t lo, uint64_t hi, F &&f)
+{
+    for (uint64_t base = lo; base < hi; base += (uint64_t)kBinThreads * kBinBatch) {
+        uint32_t lv[kBinBatch];
+#pragma unroll
+        for (int k = 0; k < kBinBatch; k++) {
+            const uint64_t i = base + (uint64_t)k * kBinThreads + threadIdx.x;
+            lv[k] = i < hi ? len[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kBinBatch; k++) {
+            const uint64_t i = base + (uint64_t)k * kBinThreads + threadIdx.x;
+            if (base + (uint64_t)k * kBinThreads >= hi) break;  // workgroup-uniform
+            f(i, i < hi, length_bucket(lv[k]));
+        }
+    }
+}
+
 // Pass 1: per-workgroup bucket counts; each workgroup reserves its slice of
 // every non-empty bucket with one atomic (offsets within the bucket).
-// gcount must be zero on entry.
-__global__ __launch_bounds__(256) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk, uint32_t *gcount,
-                                                   uint32_t *blockoff)
+// gcount must be zero on entry (k_frames_ragged re-zeroes it for the next
+// batch once pass 2 has consumed it).
+__global__ __launch_bounds__(kBinThreads) void k_bin_count(const uint32_t *len, uint32_t n, uint32_t chunk,
+                                                           uint32_t *gcount, uint32_t *blockoff)
 {
     __shared__ uint32_t cnt[kBuckets];
     for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cnt[b] = 0;
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
-    for (uint64_t base = lo; base < hi; base += blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        const bool v = i < hi;
-        (void)bucket_slot(cnt, v ? length_bucket(len[i]) : 0, v);
-    }
+    for_each_bucket(len, lo, hi, [&](uint64_t, bool v, int b) { (void)bucket_slot(cnt, v ? b : 0, v); });
     __syncthreads();
     for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
         blockoff[(size_t)blockIdx.x * kBuckets + b] = cnt[b] ? atomicAdd(&gcount[b], cnt[b]) : 0u;
 }
 
-// Pass 2 (one wave): bucket starts in sorted order (longest bucket first) by a
-// wave prefix scan, and the class table: class c occupies sorted positions
-// [cstart, cstart+ccount) and is cut into items of 64/G_c frames (one wave
-// step each); items are numbered longest class first: class c owns items
-// [istart[c], istart[c+1]). ctab = {cstart[4], ccount[4], istart[5]}.
-__global__ __launch_bounds__(64) void k_bin_plan(const uint32_t *gcount, uint32_t *bstart, uint32_t *ctab)
+// Bucket starts in sorted order (longest bucket first), by a prefix scan in
+// one wave, into bstart (LDS).
+__device__ __forceinline__ void bin_starts_wave(const uint32_t *gcount, uint32_t *bstart)
 {
     constexpr int kPer = (kBuckets + 63) / 64;
-    __shared__ uint32_t rank_pos[kBuckets + 1];  // sorted start of rank r (bucket kBuckets-1-r)
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & 63;
     uint32_t c[kPer], sum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-        const int r = l * kPer + k;
+        const int r = l * kPer + k;  // rank r = bucket kBuckets-1-r
         c[k] = r < kBuckets ? gcount[kBuckets - 1 - r] : 0u;
         sum += c[k];
     }
@@ -394,44 +412,49 @@ __global__ __launch_bounds__(64) void k_bin_plan(const uint32_t *gcount, uint32_
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         const int r = l * kPer + k;
-        if (r < kBuckets) {
-            bstart[kBuckets - 1 - r] = pos;
-            rank_pos[r] = pos;
-        }
+        if (r < kBuckets) bstart[kBuckets - 1 - r] = pos;
         pos += c[k];
     }
-    if (l == 63) rank_pos[kBuckets] = inc;
-    __syncthreads();
-    if (l != 0) return;
-    uint32_t item = 0;
-    for (int cc = kClasses - 1; cc >= 0; cc--) {  // class cc = ranks [kBuckets - first[cc+1], kBuckets - first[cc])
-        const uint32_t cstart = rank_pos[kBuckets - kClassFirstBucket[cc + 1]];
-        const uint32_t ccount = rank_pos[kBuckets - kClassFirstBucket[cc]] - cstart;
-        const uint32_t per = 64u / (uint32_t)class_lanes(cc);
-        ctab[8 + cc] = item;
-        item += (ccount + per - 1) / per;
-        ctab[cc] = ccount ? cstart : 0u;
-        ctab[4 + cc] = ccount;
-    }
-    ctab[12] = item;  // total items
 }
 
-// Pass 3: scatter frame indices into sorted order (order within a bucket is
-// unspecified; every output is written at its frame's own index).
-__global__ __launch_bounds__(256) void k_bin_scatter(const uint32_t *len, uint32_t n, uint32_t chunk,
-                                                     const uint32_t *bstart, const uint32_t *blockoff, uint32_t *order)
+// Pass 2: the plan (every workgroup scans the 136 bucket counts itself;
+// workgroup 0 also writes the class table and zeroes the work-queue heads),
+// then the frame indices are scattered into sorted order (order within a
+// bucket is unspecified; every output is written at its frame's own index).
+__global__ __launch_bounds__(kBinThreads) void k_bin_scatter(const uint32_t *len, uint32_t n, uint32_t chunk,
+                                                             const uint32_t *gcount, const uint32_t *blockoff,
+                                                             uint32_t *ctab, uint32_t *heads, uint32_t *order)
 {
     __shared__ uint32_t cur[kBuckets];
-    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x)
-        cur[b] = bstart[b] + blockoff[(size_t)blockIdx.x * kBuckets + b];
+    if (threadIdx.x < 64) bin_starts_wave(gcount, cur);
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 8u * 16u) heads[threadIdx.x] = 0u;
+        if (threadIdx.x == 0) {
+            // class cc = the sorted range from its longest bucket's start to the
+            // next shorter class's (class 0 ends at n: every frame has a bucket);
+            // items are numbered longest class first
+            uint32_t item = 0;
+            for (int cc = kClasses - 1; cc >= 0; cc--) {
+                const uint32_t cstart = cur[kClassFirstBucket[cc + 1] - 1];
+                const uint32_t cend = cc > 0 ? cur[kClassFirstBucket[cc] - 1] : n;
+                const uint32_t ccount = cend - cstart, per = 64u / (uint32_t)class_lanes(cc);
+                ctab[8 + cc] = item;
+                item += (ccount + per - 1) / per;
+                ctab[cc] = ccount ? cstart : 0u;
+                ctab[4 + cc] = ccount;
+            }
+            ctab[12] = item;  // total items
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cur[b] += blockoff[(size_t)blockIdx.x * kBuckets + b];
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = min((uint64_t)n, lo + chunk);
-    for (uint64_t base = lo; base < hi; base += blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        const bool v = i < hi;
-        const uint32_t slot = bucket_slot(cur, v ? length_bucket(len[i]) : 0, v);
+    for_each_bucket(len, lo, hi, [&](uint64_t i, bool v, int b) {
+        const uint32_t slot = bucket_slot(cur, v ? b : 0, v);
         if (v) order[slot] = (uint32_t)i;
-    }
+    });
 }
 
 // Item `it` of the ragged plan: its class and sorted-order range.
@@ -480,6 +503,7 @@ template <int PF>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
     VCRC_STAMP(0);
+    if (blockIdx.x == 0 && threadIdx.x < kBuckets) p.bin_counts[threadIdx.x] = 0u;  // consumed by k_bin_scatter
     build_lds_tables(p.consts);
     __syncthreads();
     VCRC_STAMP(1);

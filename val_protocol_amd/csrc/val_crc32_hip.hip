@@ -33,6 +33,7 @@ struct Arena {
     uint8_t *d = nullptr;
     size_t cap = 0;
     hipEvent_t last = nullptr;
+    bool counts_zero = false;  // bin scratch: bucket totals known to be zero (launch_ragged)
 };
 
 struct Ctx {
@@ -262,6 +263,7 @@ val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out)
         if (a.d) (void)hipFree(a.d);
         a.d = nullptr;
         a.cap = 0;
+        a.counts_zero = false;
         const size_t sz = std::max<size_t>(bytes, 1u << 20);
         hipError_t e = hipMalloc((void **)&a.d, sz);
         if (e != hipSuccess) return fail(VAL_ERR_NO_MEMORY, "hipMalloc(scratch)", e);
@@ -291,29 +293,33 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
     const uint32_t n = p.n;
     const uint32_t nbin = std::max(1u, std::min(1024u, (n + 2047u) / 2048u));
     const uint32_t chunk = (n + nbin - 1) / nbin;
-    // scratch: heads[8][16] u32 + gcount[kBuckets] u32 (both zeroed) | bstart[kBuckets] u32 |
-    //          ctab[16] u32 | blockoff[nbin][kBuckets] u32 | order[n] u32
+    // scratch: heads[8][16] u32 | gcount[kBuckets] u32 | ctab[16] u32 | blockoff[nbin][kBuckets] u32 |
+    //          order[n] u32. gcount is zero between batches (k_frames_ragged re-zeroes it once
+    //          k_bin_scatter has read it); heads are zeroed by k_bin_scatter.
     const size_t sz_heads = 8u * 64u, sz_gcount = (size_t)kBuckets * 4u;
-    const size_t total = sz_heads + 2 * sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
+    const size_t total = sz_heads + sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     std::lock_guard<std::recursive_mutex> lk(g_ctx.mu);
+    Arena &a = g_ctx.bin_scratch;
     uint8_t *scratch = nullptr;
-    val_status_t st = arena_acquire(g_ctx.bin_scratch, total, s, &scratch);
+    val_status_t st = arena_acquire(a, total, s, &scratch);
     if (st != VAL_OK) return st;
     uint32_t *heads = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *gcount = heads + sz_heads / 4u;
-    uint32_t *bstart = gcount + kBuckets;
-    uint32_t *ctab = bstart + kBuckets;
+    uint32_t *ctab = gcount + kBuckets;
     uint32_t *blockoff = ctab + 16;
     uint32_t *order = blockoff + (size_t)nbin * kBuckets;
-    hipError_t e = hipMemsetAsync(scratch, 0, sz_heads + sz_gcount, s);
+    // New scratch, or a batch whose launches failed part-way: zero the counts.
+    hipError_t e = a.counts_zero ? hipSuccess : hipMemsetAsync(gcount, 0, sz_gcount, s);
+    a.counts_zero = false;
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, gcount, blockoff);
-        hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(64), 0, s, gcount, bstart, ctab);
-        hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(256), 0, s, p.len, n, chunk, bstart, blockoff, order);
+        hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(kBinThreads), 0, s, p.len, n, chunk, gcount, blockoff);
+        hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(kBinThreads), 0, s, p.len, n, chunk, gcount, blockoff, ctab,
+                           heads, order);
         fill_constants(p);
         p.order = order;
         p.plan = ctab;
         p.heads = heads;
+        p.bin_counts = gcount;
         // persistent: enough waves for the items, at most one workgroup per CU
         const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
         const unsigned blocks = (unsigned)std::max<uint64_t>(
@@ -321,8 +327,9 @@ val_status_t launch_ragged(FrameParams &p, hipStream_t s)
         if (forced_prefetch() == 0) hipLaunchKernelGGL(k_frames_ragged<0>, dim3(blocks), dim3(kBlock), 0, s, p);
         else hipLaunchKernelGGL(k_frames_ragged<1>, dim3(blocks), dim3(kBlock), 0, s, p);
         e = hipGetLastError();
+        a.counts_zero = e == hipSuccess;
     }
-    st = arena_release(g_ctx.bin_scratch, s);
+    st = arena_release(a, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
     return st;
 }
