@@ -36,6 +36,14 @@ constexpr int kMaxTree = 6;            // log2(64 lanes)
 
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));  // unit loads are dword-aligned
 typedef uint32_t u32u __attribute__((aligned(1)));
+// Frame bytes are read through global-address-space pointers: from a generic
+// pointer hipcc emitted flat loads for some kernel shapes (a flat load counts
+// in both vmcnt and lgkmcnt and is waited for with both at zero).
+typedef const uint8_t __attribute__((address_space(1))) gu8;
+typedef const u32x4u __attribute__((address_space(1))) gu32x4u;
+typedef const u32u __attribute__((address_space(1))) gu32u;
+typedef const uint32_t __attribute__((address_space(1))) gu32;
+__device__ __forceinline__ gu8 *gptr(const uint8_t *p) { return (gu8 *)p; }
 
 __shared__ uint32_t s_lds[kLdsWords];
 
@@ -45,6 +53,7 @@ __device__ __forceinline__ uint32_t lds_read(uint32_t byte_addr)
 }
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const u32u *>(p); }
+__device__ __forceinline__ uint32_t ld32(gu8 *p) { return *reinterpret_cast<gu32u *>(p); }
 
 // Per-lane LDS bases of the slice tables (T3 consumes the first byte of a word).
 struct SliceBases {
@@ -106,31 +115,54 @@ constexpr uint32_t kConstWords = kConstTree + kMaxTree * 128;
 // (pair = row >> 8, byte = row & 255), half (c >> 3) & 1 ->
 // T_{3 - (2 pair + half)}[byte]. The maps are copied word for word. Every
 // thread issues all of its loads from the constant blob before it waits on any
-// of them, so the launch pays one memory latency.
-__device__ __forceinline__ void build_lds_tables(const uint32_t *consts)
+// of them, so the launch pays one memory latency. The prologue is split in
+// two so a kernel can issue its first frame loads between the halves: the
+// blob loads go first (loads complete in issue order, so waiting for them
+// does not wait for the frame data), and the HBM latency of the first round
+// runs under the LDS fill and the barrier instead of after them (with no
+// LDS-DMA in flight, __syncthreads() is a bare s_barrier: plain loads stay
+// outstanding across it).
+struct LdsImage {
+    uint32_t v[8], vm[2];
+};
+
+__device__ __forceinline__ void lds_tables_issue(const uint32_t *consts, LdsImage &im)
 {
     const uint32_t t = threadIdx.x;
     constexpr uint32_t kMapWords = kNumMaps * 128u;
-    uint32_t v[8], vm[2];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
         const uint32_t c = (uint32_t)r * kBlock + t, row = c >> 4;
         const uint32_t slot = (row >> 8) * 2u + ((c >> 3) & 1u);
-        v[r] = consts[kConstSlice + (3u - slot) * 256u + (row & 255u)];
+        im.v[r] = consts[kConstSlice + (3u - slot) * 256u + (row & 255u)];
     }
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         const uint32_t i = (uint32_t)r * kBlock + t;
-        vm[r] = i < kMapWords ? consts[kConstGap + i] : 0u;
+        im.vm[r] = i < kMapWords ? consts[kConstGap + i] : 0u;
     }
+}
+
+__device__ __forceinline__ void lds_tables_write(const LdsImage &im)
+{
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t kMapWords = kNumMaps * 128u;
     uint4 *lds4 = reinterpret_cast<uint4 *>(s_lds);
 #pragma unroll
-    for (int r = 0; r < 8; r++) lds4[(kLdsS4 / 16u) + (uint32_t)r * kBlock + t] = make_uint4(v[r], v[r], v[r], v[r]);
+    for (int r = 0; r < 8; r++)
+        lds4[(kLdsS4 / 16u) + (uint32_t)r * kBlock + t] = make_uint4(im.v[r], im.v[r], im.v[r], im.v[r]);
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         const uint32_t i = (uint32_t)r * kBlock + t;
-        if (i < kMapWords) s_lds[kLdsMaps / 4u + i] = vm[r];
+        if (i < kMapWords) s_lds[kLdsMaps / 4u + i] = im.vm[r];
     }
+}
+
+__device__ __forceinline__ void build_lds_tables(const uint32_t *consts)
+{
+    LdsImage im;
+    lds_tables_issue(consts, im);
+    lds_tables_write(im);
 }
 
 // Host: fill the constant blob (kConstWords u32).

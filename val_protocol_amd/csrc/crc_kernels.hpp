@@ -61,11 +61,11 @@ struct FrameParams {
 // unit is dword-aligned by construction (hash_frame anchors the unit grid at
 // floor4(frame end)); a dword-aligned load never crosses a page, so nothing
 // outside the buffer's pages is touched.
-__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *up)
+__device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
 {
 #pragma unroll
     for (int q = 0; q < kWords / 4; q++) {
-        const u32x4u v = *reinterpret_cast<const u32x4u *>(up + 16 * q);
+        const u32x4u v = *reinterpret_cast<gu32x4u *>(up + 16 * q);
         w[4 * q + 0] = v.x;
         w[4 * q + 1] = v.y;
         w[4 * q + 2] = v.z;
@@ -74,34 +74,47 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], const uint8_t *
 }
 
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
-// first unit, assembled word by word with the seed in frame bytes 0..3;
-// u < 0 nothing. Lg = bytes on the unit grid; Lg < 4 frames take the byte path (tiny).
-__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, const uint8_t *fp, uint32_t Lg, uint32_t pad,
-                                           uint32_t seed, bool &tiny)
+// first unit, with the seed in frame bytes 0..3; u < 0 nothing. Lg = bytes on
+// the unit grid; Lg < 4 frames take the byte path (tiny). Loads only, into
+// registers left undefined for lanes without a unit; the masks and the seed
+// are applied by unit0_finish where the words are first used. hipcc waits for
+// every outstanding load at the first use of a loaded value, and at the end
+// of a branch whose loads feed a value defined on the other path too: with
+// the masks next to the loads (and zeros on the other path) the 16 loads of
+// unit 0 ran one memory round trip after another, behind round 1's prefetch.
+// Unit u starts at fp + 64u - pad, dword-aligned (the grid ends at
+// floor4(frame end)). Unit 0 starts pad bytes before the frame: a word of it
+// wholly before the frame reads the frame's first dword, base + (pad & ~3),
+// instead (no byte outside that dword is touched) and is masked to zero.
+__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad)
 {
-    tiny = false;
-    if (u > 0) {
-        load_full(w, fp + (uint64_t)u * kUnit - pad);
-        // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
-        if (u == 1 && pad > kUnit - 4) w[0] ^= seed >> (8 * (kUnit - pad));
-    } else if (u == 0 && Lg >= 4) {
+    if (u >= 0 && Lg >= 4) {
+        gu8 *base = fp + ((int64_t)u * kUnit - pad);
+        const uint32_t lo = u == 0 ? (pad & ~3u) : 0u;
 #pragma unroll
-        for (int i = 0; i < kWords; i++) {
-            const int q = 4 * i - (int)pad;  // frame offset of this word
-            uint32_t x = 0;
-            if (q >= 0) {
-                x = ld32(fp + q);
-                if (q < 4) x ^= seed >> (8 * q);
-            } else if (q > -4) {
-                x = (ld32(fp) ^ seed) << (8 * (-q));
-            }
-            w[i] = x;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < kWords; i++) w[i] = 0;
-        tiny = (u == 0);
+        for (int i = 0; i < kWords; i++) w[i] = *reinterpret_cast<gu32 *>(base + max(4u * (uint32_t)i, lo));
     }
+}
+
+// Mask and seed of unit-0 word i (frame offset q = 4i - pad): bytes before the
+// frame are zero and the seed is XORed into frame bytes 0..3.
+__device__ __forceinline__ uint32_t unit0_word(uint32_t x, int q, uint32_t seed)
+{
+    if (q <= -4) return 0u;
+    if (q < 0) return (x & (~0u << (8 * -q))) ^ (seed << (8 * -q));
+    return q < 4 ? x ^ (seed >> (8 * q)) : x;
+}
+
+__device__ __forceinline__ void unit0_finish(uint32_t (&w)[kWords], int u, uint32_t Lg, uint32_t pad, uint32_t seed)
+{
+    const bool has = u >= 0 && Lg >= 4;
+#pragma unroll
+    for (int i = 0; i < kWords; i++) {
+        const uint32_t x = u == 0 ? unit0_word(w[i], 4 * i - (int)pad, seed) : w[i];
+        w[i] = has ? x : 0u;
+    }
+    // Seed bytes that did not fit in a unit 0 holding < 4 real bytes.
+    if (u == 1 && pad > kUnit - 4) w[0] ^= seed >> (8 * (kUnit - pad));
 }
 
 // Descriptor of frame f (offset and CRC-input length).
@@ -145,14 +158,17 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // so a wave pays one HBM latency instead of R - 1).
 // GT = 0: G is the runtime value Gr (the ragged kernel: one code path for
 // every length class, half the registers of four inlined instances).
-template <int GT, int PF>
+// pre() runs once this frame's first loads are issued and before the first
+// LDS read: a launch's first call passes the LDS fill and the barrier, so the
+// latency of round 0 runs under them.
+template <int GT, int PF, typename Pre>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           const SliceBases &sb, int Gr = GT)
+                                           const SliceBases &sb, int Gr, Pre &&pre)
 {
     constexpr int D = PF > 0 ? PF : 1;
     const int G = GT ? GT : Gr;
     const uint32_t gmap = gap_map(GT ? ilog2(GT) : __builtin_ctz((unsigned)Gr));
-    const uint8_t *fp = p.base + off;
+    gu8 *fp = gptr(p.base) + off;
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
     // The unit grid ends at floor4(frame end), so every unit is dword-aligned
     // whatever the frame's byte alignment; the tb <= 3 bytes past it are fed
@@ -160,11 +176,25 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     const uint32_t tb = min((uint32_t)((uintptr_t)(fp + L) & 3u), L);
     const uint32_t Lg = L - tb;
     const uint32_t U = Lg ? (Lg + kUnit - 1) / kUnit : 1u;
-    const uint32_t R = active ? (U + G - 1) / G : 0u;
+    const uint32_t R = active ? (U + G - 1) >> (GT ? ilog2(GT) : __builtin_ctz((unsigned)Gr)) : 0u;
     const uint32_t pad = U * kUnit - Lg;
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
-    const uint8_t *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
+    gu8 *up = fp + ((int64_t)u0 + G) * kUnit - pad;  // its unit in round 1
     const uint64_t kStep = (uint64_t)G * kUnit;                // bytes between a lane's rounds
+    // Round 0 is issued before the prefetched rounds: loads complete in issue
+    // order, so hashing it never waits for them.
+    uint32_t w0[kWords];
+    const bool tiny = u0 == 0 && Lg < 4;
+    load_unit0(w0, u0, fp, Lg, pad);
+    // header_crc: by the lane holding unit 0, from the frame's first line,
+    // which round 0 reads anyway (read after the merge, the line had left the
+    // caches: +0.4% HBM traffic on cfg3).
+    const bool hdr = R > 0 && u0 == 0 && p.out_hdr;
+    uint32_t h0, h1;
+    if (hdr && L >= 8) {
+        h0 = ld32(fp);
+        h1 = ld32(fp + 4);
+    }
     uint32_t nxt[D][kWords];
     if (PF > 0) {
 #pragma unroll
@@ -180,14 +210,12 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
     first = __builtin_amdgcn_readfirstlane(first);
-    // header_crc: by the lane holding unit 0, while the frame's first line is
-    // being read anyway (read after the merge, the line had left the caches:
-    // +0.4% HBM traffic on cfg3).
-    if (R > 0 && u0 == 0 && p.out_hdr) {
+    pre();
+    if (hdr) {
         uint32_t h = seed;
         if (L >= 8) {
-            h = s4_step(h, ld32(fp), sb);
-            h = s4_step(h, ld32(fp + 4), sb);
+            h = s4_step(h, h0, sb);
+            h = s4_step(h, h1, sb);
         } else {
             for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
         }
@@ -196,10 +224,8 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
-        uint32_t w[kWords];
-        bool tiny;
-        load_unit0(w, u0, fp, Lg, pad, seed, tiny);
-        acc = s4_words_from(first, w, sb);
+        unit0_finish(w0, u0, Lg, pad, seed);
+        acc = s4_words_from(first, w0, sb);
         if (tiny) {  // Lg < 4: state of all L bytes straight from the seed
             acc = seed;
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
@@ -235,6 +261,17 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             }
         }
     }
+    // The tb <= 3 bytes past the grid and, on verify, the stored trailer: all
+    // issued before the merge, which hides their round trip (a byte loop after
+    // it waited once per byte).
+    uint32_t tail[3] = {0, 0, 0}, trailer = 0;
+    if (active && g == G - 1) {
+        if (tb && Lg >= 4) {
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) tail[j] = fp[Lg + min(j, tb - 1)];
+        }
+        if (p.verify) trailer = ld32(fp + L);
+    }
     // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j
     // bytes (LDS nibble map: 8 lookups, where a bit-matrix product costs 96 VALU).
 #pragma unroll
@@ -246,12 +283,15 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
         acc = map_apply(left, tree_map(j)) ^ (right ? acc : other);
     }
     if (active && g == G - 1) {
-        if (Lg >= 4)  // the bytes past the unit grid (tiny frames already fed all L)
-            for (uint32_t i = Lg; i < L; i++) acc = byte_step(acc, fp[i], sb);
+        if (Lg >= 4) {  // the bytes past the unit grid (tiny frames already fed all L)
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++)
+                if (j < tb) acc = byte_step(acc, tail[j], sb);
+        }
         const uint32_t crc = acc ^ p.xorout;
         if (p.out_crc) p.out_crc[f] = crc;
         if (p.verify) {
-            const bool good = (crc == ld32(fp + L));
+            const bool good = (crc == trailer);
             if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
             if (!good && p.nbad) atomicAdd(p.nbad, 1u);
         }
@@ -277,13 +317,29 @@ __device__ uint64_t g_vcrc_time[4096 * 4];
 // a dynamic work queue that evened them out measured 3-5% slower on cfg3,
 // cfg4 and unaligned uniform batches (profiles/r01_ab_dynamic_uniform.log):
 // the static deal is kept.
+// One frame group of a uniform wave: hash group f.., fetch the next group's
+// descriptors meanwhile, advance.
+template <int G, int PF, typename Pre>
+__device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
+                                           uint64_t step, int lane, const SliceBases &sb, Pre &&pre)
+{
+    const uint64_t fn = f + step;
+    uint64_t off_n = 0;
+    uint32_t L_n = 0;
+    if (fn < p.n) frame_desc(p, fn, off_n, L_n);
+    hash_frame<G, PF>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
+    f = fn;
+    off = off_n;
+    L = L_n;
+    fb += step;
+}
+
 template <int G, int PF>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
     VCRC_STAMP(0);
-    build_lds_tables(p.consts);
-    __syncthreads();
-    VCRC_STAMP(1);
+    LdsImage im;
+    lds_tables_issue(p.consts, im);
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
@@ -293,16 +349,17 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     uint64_t fb = wave * kGroups, f = fb + (uint64_t)(lane / G), off = 0;
     uint32_t L = 0;
     if (f < p.n) frame_desc(p, f, off, L);
-    for (; fb < p.n; fb += nwaves * kGroups) {
-        const uint64_t fn = f + nwaves * kGroups;
-        uint64_t off_n = 0;
-        uint32_t L_n = 0;
-        if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-        hash_frame<G, PF>(p, f, f < p.n, off, L, lane % G, sb);
-        f = fn;
-        off = off_n;
-        L = L_n;
-    }
+    // Every wave runs the first pass (lanes past the batch hash nothing): the
+    // LDS fill and the barrier sit in its hash_frame call, after the frame
+    // loads are issued. Peeled, so the LDS image's registers are dead in the
+    // loop.
+    const LdsImage &cim = im;
+    group_pass<G, PF>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim] {
+        lds_tables_write(cim);
+        __syncthreads();
+        VCRC_STAMP(1);
+    });
+    while (fb < p.n) group_pass<G, PF>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
     VCRC_STAMP(2);
 }
 
@@ -504,6 +561,9 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
     VCRC_STAMP(0);
     if (blockIdx.x == 0 && threadIdx.x < kBuckets) p.bin_counts[threadIdx.x] = 0u;  // consumed by k_bin_scatter
+    // The first item's frame loads wait on three dependent reads (plan, sorted
+    // order, descriptors), so the LDS fill is not overlapped with them here:
+    // its registers would be live through the loop (a spill at 128 VGPRs).
     build_lds_tables(p.consts);
     __syncthreads();
     VCRC_STAMP(1);
@@ -537,7 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
         const int G = class_lanes(cur.c);
-        hash_frame<0, PF>(p, f, active, off, L, lane & (G - 1), sb, G);
+        hash_frame<0, PF>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
         if (it_n >= items) {
             VCRC_STAMP(2);
             break;
