@@ -385,11 +385,6 @@ __host__ __device__ inline int length_bucket(uint32_t L)
 }
 __host__ __device__ inline int bucket_class(int b) { return b < 8 ? 0 : b < 37 ? 1 : b < 118 ? 2 : 3; }
 constexpr int kClassFirstBucket[kClasses + 1] = {0, 8, 37, 118, kBuckets};
-// Ragged plan (u32 words): five item classes, the four length classes and the
-// tail (class 4), which re-cuts the last class's final items at twice its lanes
-// per frame, so the launch ends about half an item after the bytes run out.
-constexpr int kTail = kClasses;
-constexpr int kPlanStart = 0, kPlanCount = 5, kPlanItem0 = 10, kPlanItems = 15, kPlanTailLanes = 16, kPlanWords = 32;
 
 // A wave's lanes that all hold the same bucket (uniform batches) reserve
 // their slots with one LDS atomic; mixed waves use one atomic per lane.
@@ -494,39 +489,19 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_scatter(const uint32_t *len
         if (threadIdx.x < 8u * 16u) heads[threadIdx.x] = 0u;
         if (threadIdx.x == 0) {
             // class cc = the sorted range from its longest bucket's start to the
-            // next shorter class's (class 0 ends at n: every frame has a bucket)
-            uint32_t cs[kClasses + 1], cn[kClasses + 1], cg[kClasses + 1];
-            for (int cc = 0; cc < kClasses; cc++) {
-                cs[cc] = cur[kClassFirstBucket[cc + 1] - 1];
-                cn[cc] = (cc > 0 ? cur[kClassFirstBucket[cc] - 1] : n) - cs[cc];
-                cg[cc] = (uint32_t)class_lanes(cc);
-            }
-            // Tail: the last non-empty class (the shortest frames, hashed last)
-            // gives its final nwaves items, if it has at least twice that many,
-            // to class 4 at twice the lanes per frame.
-            cs[kTail] = cn[kTail] = cg[kTail] = 0;
-            for (int cc = 0; cc < kClasses; cc++) {
-                if (!cn[cc]) continue;
-                const uint32_t per = 64u / cg[cc];
-                if (cg[cc] < 64u && cn[cc] / per >= 2u * nwaves) {
-                    cn[kTail] = nwaves * per;
-                    cn[cc] -= cn[kTail];
-                    cs[kTail] = cs[cc] + cn[cc];
-                    cg[kTail] = 2u * cg[cc];
-                }
-                break;
-            }
-            // items are numbered longest class first, then the tail
+            // next shorter class's (class 0 ends at n: every frame has a bucket);
+            // items are numbered longest class first
             uint32_t item = 0;
-            for (int k = 0; k <= kClasses; k++) {
-                const int cc = k < kClasses ? kClasses - 1 - k : kTail;
-                ctab[kPlanStart + cc] = cn[cc] ? cs[cc] : 0u;
-                ctab[kPlanCount + cc] = cn[cc];
-                ctab[kPlanItem0 + cc] = item;
-                if (cn[cc]) item += (cn[cc] + 64u / cg[cc] - 1u) / (64u / cg[cc]);
+            for (int cc = kClasses - 1; cc >= 0; cc--) {
+                const uint32_t cstart = cur[kClassFirstBucket[cc + 1] - 1];
+                const uint32_t cend = cc > 0 ? cur[kClassFirstBucket[cc] - 1] : n;
+                const uint32_t ccount = cend - cstart, per = 64u / (uint32_t)class_lanes(cc);
+                ctab[8 + cc] = item;
+                item += (ccount + per - 1) / per;
+                ctab[cc] = ccount ? cstart : 0u;
+                ctab[4 + cc] = ccount;
             }
-            ctab[kPlanItems] = item;
-            ctab[kPlanTailLanes] = cg[kTail];
+            ctab[12] = item;  // total items
         }
     }
     __syncthreads();
