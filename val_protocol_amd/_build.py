@@ -1,10 +1,17 @@
-"""Build recipe for libval_crc_hip.so (gfx950). Invoked by __graft_entry__.build()."""
+"""Build recipe for libval_crc_hip.so (gfx950). Invoked by __graft_entry__.build()
+and, on demand, by ``crc.lib()`` when the library is missing or was built from
+other sources (a content stamp, not mtimes: a gpurun snapshot does not keep
+them)."""
 from __future__ import annotations
 
+import fcntl
+import glob
+import hashlib
 import os
 import shutil
 import subprocess
 import sys
+import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "val_protocol_amd", "csrc")
@@ -20,16 +27,74 @@ def _run(cmd, verbose):
     subprocess.run(cmd, check=True)
 
 
-def build(verbose: bool = True) -> str:
+def sources() -> list[str]:
+    """Every file the library is built from (sources, headers, this recipe)."""
+    files = sorted(glob.glob(os.path.join(CSRC, "*"))) + sorted(glob.glob(os.path.join(INC, "*.h")))
+    return [f for f in files if os.path.isfile(f)] + [os.path.abspath(__file__)]
+
+
+def source_hash() -> str:
+    h = hashlib.sha256()
+    for f in sources():
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def stamp_path(out: str) -> str:
+    return out + ".srchash"
+
+
+def is_current(out: str = OUT) -> bool:
+    """The library exists and was built from the sources in this tree."""
+    try:
+        with open(stamp_path(out)) as fh:
+            return os.path.exists(out) and fh.read().strip() == source_hash()
+    except OSError:
+        return False
+
+
+def build(verbose: bool = True, out: str = OUT, build_dir: str = BUILD) -> str:
+    """Compile val_wire.c (gcc) and val_crc32_hip.hip (hipcc, gfx950) and link
+    ``out``. The library is linked to a temporary name and renamed, so a
+    process that loads ``out`` meanwhile never sees a half-written file."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    os.makedirs(BUILD, exist_ok=True)
-    wire_o = os.path.join(BUILD, "val_wire.o")
-    hip_o = os.path.join(BUILD, "val_crc32_hip.o")
+    os.makedirs(build_dir, exist_ok=True)
+    digest = source_hash()
+    wire_o = os.path.join(build_dir, "val_wire.o")
+    hip_o = os.path.join(build_dir, "val_crc32_hip.o")
     _run(["gcc", "-O2", "-fPIC", "-std=c99", "-Wall", "-Wextra", "-Werror", f"-I{INC}", "-c",
           os.path.join(CSRC, "val_wire.c"), "-o", wire_o], verbose)
-    _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", f"-I{INC}", f"-I{CSRC}", "-c",
-          os.path.join(CSRC, "val_crc32_hip.hip"), "-o", hip_o], verbose)
-    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, hip_o, wire_o], verbose)
+    _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror", f"-I{INC}", f"-I{CSRC}",
+          "-c", os.path.join(CSRC, "val_crc32_hip.hip"), "-o", hip_o], verbose)
+    fd, tmp = tempfile.mkstemp(prefix=".libval_crc_hip.", suffix=".so", dir=os.path.dirname(out))
+    os.close(fd)
+    try:
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, hip_o, wire_o, "-lpthread"], verbose)
+        os.chmod(tmp, 0o755)
+        os.replace(tmp, out)
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+    with open(stamp_path(out), "w") as fh:
+        fh.write(digest + "\n")
+    return out
+
+
+def ensure_built(verbose: bool = False) -> str:
+    """Build OUT under a file lock unless it is current (concurrent test
+    processes build once)."""
+    if is_current():
+        return OUT
+    lock = os.path.join(os.path.dirname(OUT), ".build.lock")
+    with open(lock, "w") as fh:
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        try:
+            if not is_current():
+                build(verbose=verbose)
+        finally:
+            fcntl.flock(fh, fcntl.LOCK_UN)
     return OUT
 
 

@@ -100,9 +100,17 @@ def _declare(lib: ctypes.CDLL) -> None:
 
 
 def lib() -> ctypes.CDLL:
-    """Load the HIP shared library (raises if it was not built)."""
+    """Load the HIP shared library. A library that is missing, or was built
+    from other sources than this tree's, is (re)built first under a file lock;
+    if that fails this raises (there is no CPU fallback)."""
     global _lib
     if _lib is None:
+        from . import _build
+
+        try:
+            _build.ensure_built()
+        except Exception as e:  # noqa: BLE001 - reported with the cause
+            raise ImportError(f"{LIB_PATH} could not be built ({e}); no CPU fallback") from e
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() first (no CPU fallback)")
         try:  # one HIP runtime per process: let torch's libamdhip64 load first
