@@ -24,9 +24,18 @@
  *                              shard batches across GPUs (no reference
  *                              counterpart; zlib's crc32_combine identity)
  *
- * Every entry point computes on the GPU. There is no CPU fallback: a missing
- * device or a HIP failure returns VAL_ERR_IO (batch calls) or aborts with a
- * message (the scalar hooks, whose C signature has no error channel).
+ *   val_crc32_*_multi       -> the same batches split over several GPUs of
+ *                              one process, one host thread per device
+ *                              (a window of src/val_sender.c:
+ *                              822-841 sharded by contiguous frame ranges)
+ *
+ * Every entry point computes on the GPU. Batch calls return VAL_ERR_IO on a
+ * missing device or a HIP failure. The three scalar hooks (provider,
+ * val_crc32, val_crc32_update_state) have no error channel and are called by
+ * VAL under its session mutex on every frame, so on a GPU failure they return
+ * the CRC from this library's own CPU slice-by-8 and count it
+ * (val_gpu_cpu_fallback_count); VAL_GPU_CPU_FALLBACK=0 or
+ * val_gpu_set_cpu_fallback(0) makes them abort instead.
  */
 #ifndef VAL_CRC32_GPU_H
 #define VAL_CRC32_GPU_H
@@ -43,14 +52,29 @@ extern "C" {
 #define VAL_GPU_ABI_VERSION 1u
 
 /* ---- lifetime ---------------------------------------------------------- */
-/* Bind the calling process to HIP device `device` (0-based). Idempotent;
- * lazily called with device 0 by the first CRC call. */
+/* Initialise HIP device `device` (0-based) and bind the calling thread to it.
+ * The first device initialised is the process default, used by threads that
+ * never bound one; the first CRC call initialises device 0 if none was.
+ * Each device has its own streams, constant tables, staging and scratch. */
 val_status_t val_gpu_init(int device);
+/* Initialise devices 0..n-1 (n <= 0: all). Returns how many are usable. */
+int val_gpu_init_devices(int n);
+/* Bind the calling thread to `device` (initialised on first use); later calls
+ * of this thread run there. hipSetDevice is per thread in HIP. */
+val_status_t val_gpu_set_device(int device);
+/* Device the calling thread's calls run on (-1: none initialised yet). */
+int val_gpu_current_device(void);
+/* Release every device context of the process. */
 void val_gpu_shutdown(void);
 int val_gpu_device_count(void);
 uint32_t val_gpu_abi_version(void);
 /* Last HIP/validation error text of the calling thread ("" if none). */
 const char *val_gpu_last_error(void);
+/* Scalar-hook calls answered by the CPU because the GPU path failed. */
+uint64_t val_gpu_cpu_fallback_count(void);
+/* 1: failed scalar hooks use the CPU (default), 0: they abort, -1: from
+ * VAL_GPU_CPU_FALLBACK (unset or non-"0" = on). */
+void val_gpu_set_cpu_fallback(int enable);
 
 /* ---- scalar hooks (host memory) --------------------------------------- */
 uint32_t val_gpu_crc32_provider(uint32_t seed, const void *buf, size_t len);
@@ -107,6 +131,34 @@ val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const
 val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
                                           const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint8_t *ok,
                                           uint32_t *nbad);
+
+/* ---- several GPUs in one process ----------------------------------------
+ * The *_host batches above split into ndev shards (ndev <= 0: one per
+ * visible device): contiguous frame ranges balanced by CRC-input bytes
+ * (val_shard_frames), one host thread per shard running the single-device
+ * path on device (shard % device count);
+ * outputs are disjoint ranges of crc/hdr/ok, nbad is the sum. No collective
+ * and no peer copies: frames are independent.                           */
+val_status_t val_crc32_frames_host_multi(const uint8_t *base, uint64_t base_len, const uint64_t *off,
+                                         const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint32_t *crc,
+                                         uint32_t *hdr, int ndev);
+val_status_t val_crc32_verify_frames_host_multi(const uint8_t *base, uint64_t base_len, const uint64_t *off,
+                                                const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n,
+                                                uint8_t *ok, uint32_t *nbad, int ndev);
+/* Raw register after feeding the host window data[0, len) to state_in, the
+ * window cut into ndev 4 KiB-aligned byte ranges hashed on devices
+ * (range % device count) and
+ * folded with the GF(2) shift (val_crc32_update_state semantics). */
+val_status_t val_crc32_region_host_multi(const void *data, uint64_t len, uint32_t state_in, uint32_t *state_out,
+                                         int ndev);
+/* [*start, *start + *count) = the frames shard `rank` of `world` owns:
+ * contiguous, balanced by len[] (NULL: by count). Host only. */
+void val_shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t rank, uint32_t *start,
+                      uint32_t *count);
+/* Fold k partial raw states in order: state[0] carries the initial register,
+ * state[i] (i >= 1) covers nbytes[i] bytes from a zero register.
+ * acc = state[0]; acc = shift(acc, nbytes[i]) ^ state[i]. Host only. */
+uint32_t val_crc32_fold_partials(const uint32_t *state, const uint64_t *nbytes, uint32_t k);
 
 /* ---- pinned host staging ------------------------------------------------
  * Page-locked host memory for frame windows (e.g. the TX window staging

@@ -29,6 +29,10 @@
  *       the reference TX one frame at a time vs the batched GPU path, and
  *       received + verified by the reference RX vs scan + one GPU verify
  *       (see mode_windowbench).
+ *   provider_harness none fixtures
+ *       writes tests/golden/dropin_vectors.json (see mode_fixtures): what the
+ *       GPU drop-in tests check the product against on the GPU box, where no
+ *       reference code exists.
  *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
  *       full val_send_files / val_receive_files transfer over an in-memory
  *       duplex pipe (the reference test strategy), provider on
@@ -124,9 +128,16 @@ static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
 }
 
 typedef struct {
+    uint8_t *bytes;   /* the whole frame as sent */
+    size_t len;
+} frame_rec_t;
+
+typedef struct {
     pipe_t *out, *in;
     uint32_t digest;   /* running CRC (reference val_crc32 state) of all sent bytes */
     unsigned long frames;
+    frame_rec_t *log;  /* optional frame log (fixtures mode): one record per transport.send */
+    size_t nlog, caplog;
 } end_t;
 
 static int tp_send(void *ctx, const void *data, size_t len)
@@ -134,6 +145,16 @@ static int tp_send(void *ctx, const void *data, size_t len)
     end_t *e = (end_t *)ctx;
     e->digest = val_crc32_update_state(e->digest, data, len);
     e->frames++;
+    if (e->caplog) {
+        if (e->nlog == e->caplog) {
+            e->caplog *= 2;
+            e->log = (frame_rec_t *)realloc(e->log, e->caplog * sizeof(frame_rec_t));
+        }
+        frame_rec_t *r = &e->log[e->nlog++];
+        r->bytes = (uint8_t *)malloc(len ? len : 1);
+        memcpy(r->bytes, data, len);
+        r->len = len;
+    }
     return pipe_push(e->out, (const uint8_t *)data, len);
 }
 
@@ -602,8 +623,316 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu)
     return 0;
 }
 
+/* ---- fixtures: drop-in golden vectors, reference built-in CRC only --------
+ * `provider_harness none fixtures > tests/golden/dropin_vectors.json`.
+ * Everything the GPU drop-in tests need to check the product against the
+ * reference without running reference code on the GPU box: TX frames of
+ * val_internal_send_packet_ex, RX verdicts of val_internal_recv_packet on
+ * clean and corrupted frames, TX windows of W frames with corrupted-frame
+ * verdicts, and the F6 frame log of the 1 MiB / MTU 1024
+ * loopback transfer (BASELINE configs[0]). Payload bytes are not stored: they
+ * are oracle_prng_fill streams the tests regenerate (tests/_prng.py). */
+static void fx_hex(const uint8_t *p, size_t n) { hex(p, n); }
+
+static uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
+static uint64_t le64(const uint8_t *p) { return (uint64_t)le32(p) | (uint64_t)le32(p + 4) << 32; }
+
+static void fx_tx(void)
+{
+    const size_t mtu = VAL_MAX_PACKET_SIZE;
+    pipe_t a;
+    pipe_init(&a, 4u << 20);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, NULL);
+    val_session_t *s = NULL;
+    val_session_create(&cfg, &s, NULL);
+    const uint32_t payloads[] = {0, 1, 3, 492, 1004, 1024, 4093, 16384, 65516, 65527, 65528, 65536};
+    uint8_t *pl = (uint8_t *)malloc(70000), *w = (uint8_t *)malloc(mtu);
+    printf("\"tx\":[");
+    int first = 1;
+    for (size_t i = 0; i < sizeof(payloads) / sizeof(payloads[0]); i++)
+        for (int inc = 0; inc <= 1; inc++) {
+            const uint64_t seed = 0xF3u ^ ((uint64_t)payloads[i] << 8);
+            const uint64_t off = (uint64_t)i * 65536u + (inc ? (1ull << 32) + 5u : 0u);
+            oracle_prng_fill(seed, pl, payloads[i]);
+            size_t before = a.len;
+            int rc = val_internal_send_packet_ex(s, VAL_PKT_DATA, pl, payloads[i], off, inc);
+            size_t wl = a.len - before;
+            pipe_pop(&a, w, wl, 10);
+            printf("%s\n{\"payload_len\":%u,\"include_offset\":%d,\"offset\":%llu,\"seed\":%llu,\"rc\":%d,\"wire_len\":%zu,"
+                   "\"prefix\":",
+                   first ? "" : ",", payloads[i], inc, (unsigned long long)off, (unsigned long long)seed, rc, wl);
+            fx_hex(w, wl >= 4 ? (wl - 4 < 16 ? wl - 4 : 16) : 0);
+            printf(",\"trailer\":%u}", wl >= 4 ? le32(w + wl - 4) : 0u);
+            first = 0;
+        }
+    printf("],\n");
+    val_session_destroy(s);
+    free(pl);
+    free(w);
+}
+
+static void fx_rx(void)
+{
+    const size_t mtu = 70000;
+    pipe_t a;
+    pipe_init(&a, 8u << 20);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, NULL);
+    val_session_t *s = NULL;
+    val_session_create(&cfg, &s, NULL);
+    const uint32_t payloads[] = {0, 7, 1004, 16384, 65516};
+    uint8_t *pl = (uint8_t *)malloc(70000), *out = (uint8_t *)malloc(70000);
+    int idx = 0;
+    printf("\"rx\":[");
+    for (size_t i = 0; i < sizeof(payloads) / sizeof(payloads[0]); i++)
+        for (int corrupt = 0; corrupt <= 3; corrupt++) {
+            const uint64_t seed = 0xA0u + (uint64_t)idx;
+            oracle_prng_fill(seed, pl, payloads[i]);
+            val_session_t *txs = NULL;
+            val_session_create(&cfg, &txs, NULL);
+            size_t before = a.len;
+            val_internal_send_packet_ex(txs, VAL_PKT_DATA, pl, payloads[i], 4096u * (uint64_t)idx, 1);
+            size_t wl = a.len - before;
+            val_session_destroy(txs);
+            const uint32_t trailer = (uint32_t)a.buf[(a.head + before + wl - 4) % a.cap] |
+                                     (uint32_t)a.buf[(a.head + before + wl - 3) % a.cap] << 8 |
+                                     (uint32_t)a.buf[(a.head + before + wl - 2) % a.cap] << 16 |
+                                     (uint32_t)a.buf[(a.head + before + wl - 1) % a.cap] << 24;
+            /* 1: trailer bit, 2: content bit, 3: header (content_len kept, type_data bit) */
+            size_t pos = 0;
+            const uint8_t mask = 0x20;
+            if (corrupt) {
+                pos = corrupt == 1 ? wl - 1 : corrupt == 2 ? 8u + (wl - 12u) / 2u : 5u;
+                a.buf[(a.head + before + pos) % a.cap] ^= mask;
+            }
+            uint32_t plen = 0;
+            uint64_t off = 0;
+            val_packet_type_t t = 0;
+            int rc = val_internal_recv_packet(s, &t, out, 70000, &plen, &off, 100);
+            val_metrics_t m;
+            memset(&m, 0, sizeof m);
+            val_get_metrics(s, &m);
+            int same = (rc == VAL_OK) ? (plen == payloads[i] && memcmp(out, pl, plen) == 0) : 0;
+            printf("%s\n{\"payload_len\":%u,\"seed\":%llu,\"offset\":%llu,\"trailer\":%u,\"corrupt\":%d,\"pos\":%zu,\"mask\":%u,"
+                   "\"rc\":%d,\"payload_ok\":%d,\"crc_errors\":%u}",
+                   idx ? "," : "", payloads[i], (unsigned long long)seed, 4096ull * (unsigned long long)idx, trailer, corrupt,
+                   pos, corrupt ? mask : 0u, rc, same, m.crc_errors);
+            idx++;
+        }
+    printf("],\n");
+    val_session_destroy(s);
+    free(pl);
+    free(out);
+}
+
+/* One TX window of W frames (sender layout, src/val_sender.c:271-277,833), as
+ * mode_window, reference only. */
+static void fx_window(uint32_t W, size_t mtu, int last)
+{
+    const size_t maxp = mtu - 12;
+    const uint64_t file_size = (uint64_t)W * maxp - 777u;
+    const uint64_t file_seed = 0x3171D0;
+    uint8_t *file = (uint8_t *)malloc(file_size);
+    oracle_prng_fill(file_seed, file, file_size);
+    uint64_t *pay_off = calloc(W, 8);
+    uint32_t *pay_len = calloc(W, 4);
+    uint8_t *inc = calloc(W, 1);
+    uint32_t nf = 0;
+    for (uint64_t pos = 0; pos < file_size && nf < W; nf++) {
+        inc[nf] = (nf % 5 == 0);
+        size_t take = maxp - (inc[nf] ? 8u : 0u);
+        if (take > file_size - pos) take = (size_t)(file_size - pos);
+        pay_off[nf] = pos;
+        pay_len[nf] = (uint32_t)take;
+        pos += take;
+    }
+    pipe_t a;
+    pipe_init(&a, (size_t)W * mtu + 4096);
+    end_t e = {&a, &a, 0xFFFFFFFFu, 0};
+    val_config_t cfg;
+    make_cfg(&cfg, &e, mtu, NULL);
+    val_session_t *s = NULL;
+    val_session_create(&cfg, &s, NULL);
+    for (uint32_t i = 0; i < nf; i++) val_internal_send_packet_ex(s, VAL_PKT_DATA, file + pay_off[i], pay_len[i], pay_off[i], inc[i]);
+    const size_t ref_len = a.len;
+    uint8_t *ref = (uint8_t *)malloc(ref_len);
+    pipe_pop(&a, ref, ref_len, 10);
+    printf("{\"W\":%u,\"mtu\":%zu,\"file_seed\":%llu,\"file_size\":%llu,\"frames\":[", W, mtu, (unsigned long long)file_seed,
+           (unsigned long long)file_size);
+    for (uint32_t i = 0; i < nf; i++)
+        printf("%s[%llu,%u,%u]", i ? "," : "", (unsigned long long)pay_off[i], pay_len[i], inc[i]);
+    /* frame offsets in the stream from the headers; trailers; stream digest */
+    uint64_t *fo = calloc(nf, 8);
+    uint32_t *cl = calloc(nf, 4);
+    size_t p = 0;
+    printf("],\"trailers\":[");
+    for (uint32_t i = 0; i < nf; i++) {
+        fo[i] = p;
+        cl[i] = 8u + ((uint32_t)ref[p + 2] | (uint32_t)ref[p + 3] << 8);
+        printf("%s%u", i ? "," : "", le32(ref + p + cl[i]));
+        p += cl[i] + 4u;
+    }
+    printf("],\"wire_bytes\":%zu,\"wire_crc\":%u,\"corrupt\":[", ref_len, val_crc32(ref, ref_len));
+    int firstc = 1;
+    for (uint32_t i = 3; i < nf; i += 7) {
+        const size_t pos = fo[i] + 8u + (i * 13u) % (cl[i] - 8u);
+        const uint8_t mask = (uint8_t)(1u << (i % 8));
+        ref[pos] ^= mask;
+        printf("%s[%u,%zu,%u]", firstc ? "" : ",", i, pos, mask);
+        firstc = 0;
+    }
+    pipe_push(&a, ref, ref_len);
+    val_config_t rcfg;
+    make_cfg(&rcfg, &e, mtu, NULL);
+    val_session_t *r = NULL;
+    val_session_create(&rcfg, &r, NULL);
+    uint8_t *out = (uint8_t *)malloc(mtu);
+    printf("],\"ref_rc\":[");
+    for (uint32_t i = 0; i < nf; i++) {
+        val_packet_type_t t = 0;
+        uint32_t plen = 0;
+        uint64_t off = 0;
+        int rc = val_internal_recv_packet(r, &t, out, (uint32_t)mtu, &plen, &off, 100);
+        printf("%s%d", i ? "," : "", rc);
+    }
+    val_metrics_t m;
+    memset(&m, 0, sizeof m);
+    val_get_metrics(r, &m);
+    printf("],\"ref_crc_errors\":%u}%s\n", m.crc_errors, last ? "" : ",");
+    val_session_destroy(s);
+    val_session_destroy(r);
+    free(file);
+    free(ref);
+    free(out);
+    free(fo);
+    free(cl);
+    free(pay_off);
+    free(pay_len);
+    free(inc);
+}
+
+/* F6: the frame log of both sessions' transport.send during a 1 MiB / MTU
+ * 1024 loopback (reference harness unit_tests/send_receive/test_single_file.c:
+ * 9-11,155-161). Per frame: [type, wire_len, trailer, file_off, prefix_hex]:
+ * DATA frames (type 5) carry the first 8 (implied offset) or 16 bytes and the
+ * file offset of their payload (-1 otherwise); other frames carry every byte
+ * but the trailer. */
+static void fx_log(const end_t *e, const uint8_t *file, size_t bytes)
+{
+    uint64_t next = 0;
+    for (size_t i = 0; i < e->nlog; i++) {
+        const uint8_t *f = e->log[i].bytes;
+        const size_t wl = e->log[i].len;
+        const uint32_t content = (uint32_t)f[2] | (uint32_t)f[3] << 8;
+        long long foff = -1;
+        size_t pre = wl - 4;
+        if (f[0] == VAL_PKT_DATA) {
+            const int explicit_off = f[1] & 1u;
+            const uint64_t off = explicit_off ? le64(f + 8) : next;
+            const uint32_t plen = content - (explicit_off ? 8u : 0u);
+            const uint8_t *pay = f + 8 + (explicit_off ? 8 : 0);
+            if (off + plen > bytes || memcmp(pay, file + off, plen) != 0) {
+                fprintf(stderr, "fixtures: DATA frame %zu payload is not file[%llu:+%u]\n", i, (unsigned long long)off, plen);
+                exit(3);
+            }
+            foff = (long long)off;
+            next = off + plen;
+            pre = explicit_off ? 16 : 8;
+        }
+        printf("%s\n[%u,%zu,%u,%lld,", i ? "," : "", f[0], wl, le32(f + wl - 4), foff);
+        fx_hex(f, pre);
+        putchar(']');
+    }
+}
+
+static int mode_fixtures(void)
+{
+    printf("{\"generator\":\"oracle/provider_harness none fixtures (reference src/ built by oracle/Makefile, built-in CRC)\",\n");
+    fx_tx();
+    fx_rx();
+    printf("\"windows\":[\n");
+    fx_window(64, 1024, 0);
+    fx_window(33, 16404, 0);
+    fx_window(16, 65536, 0);
+    fx_window(7, 512, 0);
+    fx_window(300, 1024, 1);
+    printf("],\n");
+    /* F6 loopback, reference CRC on both sessions */
+    const size_t bytes = 1048576, mtu = 1024;
+    char tmpl[] = "/tmp/valfxXXXXXX";
+    char *dir = mkdtemp(tmpl);
+    if (!dir) return 2;
+    /* relative paths: the META frame carries the sender path, so the log
+       must not depend on the temporary directory's name */
+    char cwd[1024];
+    if (!getcwd(cwd, sizeof cwd) || chdir(dir) != 0) return 2;
+    const char *in = "input.bin", *outdir = "out", *out = "out/input.bin";
+    mkdir(outdir, 0777);
+    uint8_t *data = (uint8_t *)malloc(bytes);
+    oracle_prng_fill(0x10AD, data, bytes);
+    FILE *f = fopen(in, "wb");
+    fwrite(data, 1, bytes, f);
+    fclose(f);
+    pipe_t a2b, b2a;
+    pipe_init(&a2b, 64u << 20);
+    pipe_init(&b2a, 64u << 20);
+    end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0, NULL, 0, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0, NULL, 0, 0};
+    etx.caplog = erx.caplog = 4096;
+    etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
+    erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
+    val_config_t ctx_, crx;
+    make_cfg(&ctx_, &etx, mtu, NULL);
+    make_cfg(&crx, &erx, mtu, NULL);
+    val_session_t *tx = NULL, *rx = NULL;
+    if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
+    rx_job_t job = {rx, outdir, VAL_OK};
+    pthread_t th;
+    pthread_create(&th, NULL, rx_main, &job);
+    const char *files[1] = {in};
+    val_status_t st = val_send_files(tx, files, 1, NULL);
+    pthread_join(th, NULL);
+    val_metrics_t mt, mr;
+    memset(&mt, 0, sizeof mt);
+    memset(&mr, 0, sizeof mr);
+    val_get_metrics(tx, &mt);
+    val_get_metrics(rx, &mr);
+    int equal = 0;
+    FILE *g = fopen(out, "rb");
+    if (g) {
+        uint8_t *back = (uint8_t *)malloc(bytes + 1);
+        size_t r = fread(back, 1, bytes + 1, g);
+        fclose(g);
+        equal = (r == bytes) && memcmp(back, data, bytes) == 0;
+        free(back);
+    }
+    if (st != VAL_OK || job.st != VAL_OK || !equal || mt.retransmits + mr.retransmits || mt.timeouts + mr.timeouts) {
+        fprintf(stderr, "fixtures: loopback not clean (tx %d rx %d equal %d)\n", st, job.st, equal);
+        return 4;
+    }
+    printf("\"loopback\":{\"bytes\":%zu,\"mtu\":%zu,\"file_seed\":%d,\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,"
+           "\"file_crc\":%u,\"tx_digest\":%u,\"rx_digest\":%u,\"tx_frames\":[",
+           bytes, mtu, 0x10AD, mt.crc_errors, mr.crc_errors, val_crc32(data, bytes), etx.digest ^ 0xFFFFFFFFu,
+           erx.digest ^ 0xFFFFFFFFu);
+    fx_log(&etx, data, bytes);
+    printf("],\"rx_frames\":[");
+    fx_log(&erx, data, bytes);
+    printf("]}}\n");
+    val_session_destroy(tx);
+    val_session_destroy(rx);
+    remove(out);
+    remove(in);
+    rmdir(outdir);
+    if (chdir(cwd) != 0) return 5;
+    rmdir(dir);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
     if (argc < 3) {
         fprintf(stderr, "usage: %s <libval_crc_hip.so|none> tx|rx|loopback [bytes mtu]\n", argv[0]);
         return 1;

@@ -19,3 +19,22 @@ def golden():
 
     with open(os.path.join(ROOT, "tests", "golden", "ref_vectors.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_results_came_from_the_gpu(request):
+    """Every -m gpu test: the scalar hooks' CPU fallback (used only when the
+    GPU path fails) must not have answered anything during the test."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+
+    if not torch.cuda.is_available():
+        yield
+        return
+    import val_protocol_amd.crc as vc
+
+    before = vc.cpu_fallback_count()
+    yield
+    assert vc.cpu_fallback_count() == before, "a scalar hook fell back to the CPU during a GPU test"

@@ -1,6 +1,10 @@
-"""World-size-2 gloo run of the sharding logic used by bench.py --gpus N:
-frames split by bytes with no overlap/gap, and a long window split into byte
-ranges whose partial states fold (product GF(2) shift) to the oracle CRC."""
+"""World-size-2 gloo run of the sharding logic used by bench.py --gpus N and
+by the product's *_host_multi calls: frames split by bytes with no overlap or
+gap (the product's val_shard_frames), and a long window split into byte
+ranges whose partial states fold with the product's val_crc32_fold_partials to
+the oracle CRC. Without a GPU the per-rank partial states come from the
+oracle; tests/test_gpu_multi.py runs the same split and fold with partial
+states the GPU computed."""
 import os
 
 import numpy as np
@@ -30,7 +34,6 @@ def _worker(rank, world, port, data, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from tests import _oracle
-    import val_protocol_amd.crc as vc
 
     start, cnt = shard_region(data.size, world, rank, align=64)
     st = _oracle.update_state(0xFFFFFFFF if rank == 0 else 0, data[start:start + cnt])
@@ -39,7 +42,7 @@ def _worker(rank, world, port, data, q):
     dist.all_gather(out, t)  # host-side metadata only (2 words per rank)
     if rank == 0:
         parts = [(int(o[0]), int(o[1])) for o in out]
-        q.put(fold_partials(parts, vc.crc32_shift) ^ 0xFFFFFFFF)
+        q.put(fold_partials(parts) ^ 0xFFFFFFFF)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -59,3 +62,28 @@ def test_region_split_fold_gloo(world):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) == _oracle.crc32(data)
+
+
+def test_fold_partials_matches_oracle_any_split():
+    """The product's host fold over uneven splits (including empty ranges)."""
+    from tests import _oracle, _prng
+
+    data = _prng.prng_bytes(0xF01D, 300_001)
+    for cuts in ([0, 300_001], [0, 1, 300_001], [0, 4096, 4096, 150_000, 300_001], [0, 299_999, 300_001]):
+        parts = [(_oracle.update_state(0xFFFFFFFF if k == 0 else 0, data[a:b]), b - a)
+                 for k, (a, b) in enumerate(zip(cuts, cuts[1:]))]
+        assert fold_partials(parts) ^ 0xFFFFFFFF == _oracle.crc32(data)
+
+
+def test_shard_frames_matches_reference_split_rule():
+    """val_shard_frames cut r = first frame whose byte prefix reaches total*r/world."""
+    rng = np.random.default_rng(9)
+    for n, w in [(1, 8), (5, 8), (1000, 3), (262144, 8)]:
+        lens = rng.integers(0, 65532, n).astype(np.uint64)
+        csum = np.concatenate([[0], np.cumsum(lens)])
+        total = int(csum[-1])
+        for r in range(w):
+            s, c = shard_frames(n, w, r, lens)
+            want_s = 0 if r == 0 else int(np.searchsorted(csum, (total * r) // w, side="left"))
+            want_e = n if r == w - 1 else int(np.searchsorted(csum, (total * (r + 1)) // w, side="left"))
+            assert (s, s + c) == (want_s, max(want_s, want_e))

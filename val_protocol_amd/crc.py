@@ -43,7 +43,9 @@ EXPORTS = (
     "val_crc32_region_scratch_bytes", "val_crc32_frames_host", "val_crc32_verify_frames_host",
     "val_serialize_frame_header", "val_deserialize_frame_header", "val_frame_data_batch",
     "val_frame_put_trailers", "val_frame_scan", "val_gpu_host_alloc", "val_gpu_host_free",
-    "val_gpu_set_host_chunk_bytes",
+    "val_gpu_set_host_chunk_bytes", "val_gpu_init_devices", "val_gpu_set_device", "val_gpu_current_device",
+    "val_gpu_cpu_fallback_count", "val_gpu_set_cpu_fallback", "val_crc32_frames_host_multi",
+    "val_crc32_verify_frames_host_multi", "val_crc32_region_host_multi", "val_shard_frames", "val_crc32_fold_partials",
 )
 
 
@@ -97,6 +99,16 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_gpu_host_alloc", _vp, sz)
     fn("val_gpu_host_free", None, _vp)
     fn("val_gpu_set_host_chunk_bytes", i32, sz)
+    fn("val_gpu_init_devices", ctypes.c_int, ctypes.c_int)
+    fn("val_gpu_set_device", i32, ctypes.c_int)
+    fn("val_gpu_current_device", ctypes.c_int)
+    fn("val_gpu_cpu_fallback_count", u64)
+    fn("val_gpu_set_cpu_fallback", None, ctypes.c_int)
+    fn("val_crc32_frames_host_multi", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp, ctypes.c_int)
+    fn("val_crc32_verify_frames_host_multi", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp, ctypes.c_int)
+    fn("val_crc32_region_host_multi", i32, _vp, u64, u32, _vp, ctypes.c_int)
+    fn("val_shard_frames", None, u32, _vp, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32))
+    fn("val_crc32_fold_partials", u32, _vp, _vp, u32)
 
 
 def lib() -> ctypes.CDLL:
@@ -150,9 +162,39 @@ def device_count() -> int:
     return int(lib().val_gpu_device_count())
 
 
+def init_devices(n: int = 0) -> int:
+    """Initialise devices 0..n-1 (0: all); returns how many are usable."""
+    return int(lib().val_gpu_init_devices(n))
+
+
+def set_device(device: int) -> None:
+    """Bind the calling thread's later calls to `device`."""
+    _check(lib().val_gpu_set_device(device), "val_gpu_set_device")
+
+
+def current_device() -> int:
+    return int(lib().val_gpu_current_device())
+
+
+def cpu_fallback_count() -> int:
+    """Scalar-hook calls the C library answered on the CPU after a GPU failure."""
+    return int(lib().val_gpu_cpu_fallback_count())
+
+
+def _scalar(fn, *args) -> int:
+    """Call a scalar hook and fail loudly if it did not run on the GPU (the C
+    hooks fall back to the CPU because crc32_func_t has no error channel; this
+    Python API has one)."""
+    before = cpu_fallback_count()
+    r = int(fn(*args))
+    if cpu_fallback_count() != before:
+        raise ValError(VAL_ERR_IO, fn.__name__, "GPU path failed: " + last_error())
+    return r
+
+
 def val_crc32(data) -> int:
     p, n, keep = _buf(data)
-    return int(lib().val_crc32(p, n))
+    return _scalar(lib().val_crc32, p, n)
 
 
 def val_crc32_init_state() -> int:
@@ -161,7 +203,7 @@ def val_crc32_init_state() -> int:
 
 def val_crc32_update_state(state: int, data) -> int:
     p, n, keep = _buf(data)
-    return int(lib().val_crc32_update_state(state & 0xFFFFFFFF, p, n))
+    return _scalar(lib().val_crc32_update_state, state & 0xFFFFFFFF, p, n)
 
 
 def val_crc32_finalize_state(state: int) -> int:
@@ -170,7 +212,7 @@ def val_crc32_finalize_state(state: int) -> int:
 
 def crc32_provider(seed: int, data) -> int:
     p, n, keep = _buf(data)
-    return int(lib().val_gpu_crc32_provider(seed & 0xFFFFFFFF, p, n))
+    return _scalar(lib().val_gpu_crc32_provider, seed & 0xFFFFFFFF, p, n)
 
 
 def provider_address() -> int:
@@ -340,3 +382,53 @@ def verify_frames_host(base: np.ndarray, off: Optional[np.ndarray] = None, lengt
     if st not in (VAL_OK, VAL_ERR_CRC):
         _check(st, "val_crc32_verify_frames_host")
     return st, ok, int(nbad.value)
+
+
+# ---- several GPUs in one process --------------------------------
+def _host_desc(base, off, length):
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+    return base, off, length
+
+
+def frames_host_multi(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
+                      stride: int = 0, flen: int = 0, n: Optional[int] = None, header: bool = False, ndev: int = 0):
+    """frames_host split over devices 0..ndev-1 (0: all), one host thread each."""
+    base, off, length = _host_desc(base, off, length)
+    if off is not None:
+        n = off.size
+    crc = np.zeros(n, dtype=np.uint32)
+    hdr = np.zeros(n, dtype=np.uint32) if header else None
+    st = lib().val_crc32_frames_host_multi(base.ctypes.data, base.size, off.ctypes.data if off is not None else None,
+                                           length.ctypes.data if length is not None else None, stride, flen, n,
+                                           crc.ctypes.data, hdr.ctypes.data if hdr is not None else None, ndev)
+    _check(st, "val_crc32_frames_host_multi")
+    return (crc, hdr) if header else crc
+
+
+def verify_frames_host_multi(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
+                             stride: int = 0, flen: int = 0, n: Optional[int] = None, ndev: int = 0):
+    """Returns (status, ok uint8 array, nbad); status VAL_ERR_CRC on mismatch."""
+    base, off, length = _host_desc(base, off, length)
+    if off is not None:
+        n = off.size
+    ok = np.zeros(n, dtype=np.uint8)
+    nbad = ctypes.c_uint32(0)
+    st = lib().val_crc32_verify_frames_host_multi(base.ctypes.data, base.size,
+                                                  off.ctypes.data if off is not None else None,
+                                                  length.ctypes.data if length is not None else None, stride, flen,
+                                                  n, ok.ctypes.data, ctypes.byref(nbad), ndev)
+    if st not in (VAL_OK, VAL_ERR_CRC):
+        _check(st, "val_crc32_verify_frames_host_multi")
+    return st, ok, int(nbad.value)
+
+
+def region_host_multi(data, state_in: int = 0xFFFFFFFF, ndev: int = 0) -> int:
+    """Raw register of a host window hashed as ndev byte ranges on ndev GPUs."""
+    p, n, keep = _buf(data)
+    out = ctypes.c_uint32(0)
+    _check(lib().val_crc32_region_host_multi(p, n, state_in & 0xFFFFFFFF, ctypes.byref(out), ndev),
+           "val_crc32_region_host_multi")
+    return int(out.value)
