@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--verify", action="store_true", help="time the RX verify kernel instead of TX")
+    ap.add_argument("--pay", action="store_true", help="with --verify: also emit payload states (RX file-CRC by-product)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--host-inclusive", action="store_true", help="also time H2D+kernel+D2H (stderr)")
@@ -198,6 +199,7 @@ def main():
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    pay = torch.empty(n, dtype=torch.int32, device=dev) if args.pay else None
     nbad = torch.zeros(1, dtype=torch.int32, device=dev)
     kw = dict(off=d_off, length=d_len, n=n, len_hint=len_hint) if ragged else dict(stride=stride, flen=flen, n=n)
     if args.verify:  # trailers must be valid first
@@ -209,7 +211,9 @@ def main():
             buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
 
     def step():
-        if args.verify:
+        if args.verify and args.pay:
+            vc.verify_frames_ex(flat, out_ok=ok, nbad=nbad, out_hdr=hdr, out_pay=pay, **kw)
+        elif args.verify:
             vc.verify_frames(flat, out_ok=ok, nbad=nbad, out_hdr=hdr, **kw)
         else:
             vc.frames(flat, out_crc=crc, out_hdr=hdr, **kw)
@@ -329,7 +333,8 @@ def main():
                                 if ragged else f"{payload} B payload")
                              + (f" (one file, sharded over {world} GPU{'s' if world > 1 else ''}), " if strong else " per GPU, ")
                              + f"{'header_crc + ' if header else ''}trailer CRC-32"
-                             f"{' (RX verify)' if args.verify else ''}"),
+                             f"{' (RX verify)' if args.verify else ''}"
+                             f"{' + payload states' if args.pay else ''}"),
                 "frames_per_gpu": n,
                 **({"frames_total": n_total} if strong else {}),
                 "crc_input_bytes_per_frame": (bytes_per_launch / n) if ragged else flen,

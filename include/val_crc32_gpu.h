@@ -106,6 +106,19 @@ val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *
                                          uint64_t stride, uint32_t flen, uint32_t n, uint32_t len_hint, uint8_t *d_ok,
                                          uint32_t *d_nbad, uint32_t *d_crc, uint32_t *d_hdr, void *stream);
 
+/* RX verify plus the receiver's rolling file-CRC input as a by-product
+ * (reference src/val_receiver.c:794,891,1004-1005, where
+ * every in-order DATA payload goes through val_crc32_update_state): as
+ * val_crc32_verify_frames_dev, and d_pay[i] (nullable) = the raw register
+ * after feeding frame i's payload to a ZERO register. The payload is the CRC
+ * input after the 8-byte header and, when flags (byte 1) has
+ * VAL_DATA_OFFSET_PRESENT, the 8-byte offset (0 if the frame is shorter).
+ * Fold the states into the file CRC with val_crc32_fold_payload_states. */
+val_status_t val_crc32_verify_frames_ex_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                                            uint64_t stride, uint32_t flen, uint32_t n, uint32_t len_hint,
+                                            uint8_t *d_ok, uint32_t *d_nbad, uint32_t *d_crc, uint32_t *d_hdr,
+                                            uint32_t *d_pay, void *stream);
+
 /* Region CRC of one long device buffer: *d_state_out = raw register after
  * feeding d_ptr[0, len) to `state_in` (val_crc32_update_state semantics;
  * finalize with ^0xFFFFFFFF). Windows up to 64 KiB are one launch; longer
@@ -131,6 +144,18 @@ val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const
 val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
                                           const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint8_t *ok,
                                           uint32_t *nbad);
+
+/* Host-memory form of val_crc32_verify_frames_ex_dev (pay: n entries, nullable). */
+val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
+                                             const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n,
+                                             uint8_t *ok, uint32_t *nbad, uint32_t *pay);
+/* The receiver's rolling CRC over frames 0..n-1 in order, stopping before the
+ * first frame with ok[i] == 0 (ok nullable = all): for each frame
+ * state = shift(state, pay_len[i]) ^ pay_state[i], i.e.
+ * val_crc32_update_state(state, payload_i) without touching the bytes again.
+ * *n_folded (nullable) = frames folded. Host only (no GPU call). */
+uint32_t val_crc32_fold_payload_states(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len,
+                                       const uint8_t *ok, uint32_t n, uint32_t *n_folded);
 
 /* ---- several GPUs in one process ----------------------------------------
  * The *_host batches above split into ndev shards (ndev <= 0: one per

@@ -71,6 +71,16 @@ void val_frame_put_trailers(uint8_t *stream, const uint64_t *frame_off, const ui
 val_status_t val_frame_scan(const uint8_t *stream, size_t len, size_t mtu, uint32_t max_frames, uint64_t *frame_off,
                             uint32_t *crc_len, uint32_t *n_frames, size_t *consumed);
 
+/*
+ * Payload length of each scanned frame: CRC input minus the 8-byte header
+ * and, when flags has VAL_DATA_OFFSET_PRESENT, the 8-byte file offset (the
+ * bytes the receiver writes and feeds to its rolling CRC, reference
+ * src/val_receiver.c:880-891); 0 for a frame shorter than that prefix.
+ * Pairs with the payload states of val_crc32_verify_frames_ex_*.
+ */
+void val_frame_payload_lens(const uint8_t *stream, const uint64_t *frame_off, const uint32_t *crc_len, uint32_t n,
+                            uint32_t *pay_len);
+
 #ifdef __cplusplus
 }
 #endif

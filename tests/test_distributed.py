@@ -87,3 +87,23 @@ def test_shard_frames_matches_reference_split_rule():
             want_s = 0 if r == 0 else int(np.searchsorted(csum, (total * r) // w, side="left"))
             want_e = n if r == w - 1 else int(np.searchsorted(csum, (total * (r + 1)) // w, side="left"))
             assert (s, s + c) == (want_s, max(want_s, want_e))
+
+
+def test_fold_payload_states_host():
+    """The product's host fold of payload states (f4) with oracle states: the
+    rolling CRC over the concatenated payloads, stopping at the first
+    rejected frame."""
+    import val_protocol_amd.crc as vc
+    from tests import _oracle, _prng
+
+    rng = np.random.default_rng(4)
+    lens = np.concatenate([rng.integers(0, 3000, 200), [0, 0, 65516, 1, 65516]]).astype(np.uint32)
+    data = _prng.prng_bytes(41, int(lens.sum()))
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    states = np.array([_oracle.update_state(0, data[offs[i]:offs[i + 1]]) for i in range(lens.size)], np.uint32)
+    st, nf = vc.fold_payload_states(0xFFFFFFFF, states, lens)
+    assert nf == lens.size and st ^ 0xFFFFFFFF == _oracle.crc32(data)
+    ok = np.ones(lens.size, np.uint8)
+    ok[150] = 0
+    st, nf = vc.fold_payload_states(0x1234, states, lens, ok)
+    assert nf == 150 and st == _oracle.update_state(0x1234, data[:offs[150]])

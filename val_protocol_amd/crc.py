@@ -46,6 +46,8 @@ EXPORTS = (
     "val_gpu_set_host_chunk_bytes", "val_gpu_init_devices", "val_gpu_set_device", "val_gpu_current_device",
     "val_gpu_cpu_fallback_count", "val_gpu_set_cpu_fallback", "val_crc32_frames_host_multi",
     "val_crc32_verify_frames_host_multi", "val_crc32_region_host_multi", "val_shard_frames", "val_crc32_fold_partials",
+    "val_crc32_verify_frames_ex_dev", "val_crc32_verify_frames_ex_host", "val_crc32_fold_payload_states",
+    "val_frame_payload_lens",
 )
 
 
@@ -109,6 +111,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_crc32_region_host_multi", i32, _vp, u64, u32, _vp, ctypes.c_int)
     fn("val_shard_frames", None, u32, _vp, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32))
     fn("val_crc32_fold_partials", u32, _vp, _vp, u32)
+    fn("val_crc32_verify_frames_ex_dev", i32, _vp, _vp, _vp, u64, u32, u32, u32, _vp, _vp, _vp, _vp, _vp, _vp)
+    fn("val_crc32_verify_frames_ex_host", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp, _vp)
+    fn("val_crc32_fold_payload_states", u32, u32, _vp, _vp, _vp, u32, ctypes.POINTER(u32))
+    fn("val_frame_payload_lens", None, _vp, _vp, _vp, u32, _vp)
 
 
 def lib() -> ctypes.CDLL:
@@ -304,6 +310,29 @@ def verify_frames(base, *, off=None, length=None, stride: int = 0, flen: int = 0
     return out_ok, nbad
 
 
+def verify_frames_ex(base, *, off=None, length=None, stride: int = 0, flen: int = 0, n: Optional[int] = None,
+                     out_ok=None, nbad=None, out_crc=None, out_hdr=None, out_pay=None, len_hint: int = 0,
+                     stream=None):
+    """RX verify with the payload-state by-product (f4). Returns (ok, nbad, pay)
+    with pay an int32 tensor of raw zero-init payload registers."""
+    import torch
+
+    if n is None:
+        n = int(off.numel()) if off is not None else 0
+    dev = base.device
+    if out_ok is None:
+        out_ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    if nbad is None:
+        nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    if out_pay is None:
+        out_pay = torch.empty(n, dtype=torch.int32, device=dev)
+    st = lib().val_crc32_verify_frames_ex_dev(_dptr(base), _dptr(off), _dptr(length), stride, flen, n, len_hint,
+                                              _dptr(out_ok), _dptr(nbad), _dptr(out_crc), _dptr(out_hdr),
+                                              _dptr(out_pay), _stream_ptr(stream))
+    _check(st, "val_crc32_verify_frames_ex_dev")
+    return out_ok, nbad, out_pay
+
+
 def region(buf, state_in: int = 0xFFFFFFFF, out=None, stream=None):
     """Raw register after feeding the whole uint8 GPU tensor ``buf``."""
     import torch
@@ -340,6 +369,37 @@ class PinnedBuffer:
             self.free()
         except Exception:
             pass
+
+
+def verify_frames_ex_host(base: np.ndarray, off: Optional[np.ndarray] = None, length: Optional[np.ndarray] = None,
+                          stride: int = 0, flen: int = 0, n: Optional[int] = None):
+    """Returns (status, ok, nbad, pay uint32 array of payload states)."""
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        n = off.size
+    ok = np.zeros(n, dtype=np.uint8)
+    pay = np.zeros(n, dtype=np.uint32)
+    nbad = ctypes.c_uint32(0)
+    st = lib().val_crc32_verify_frames_ex_host(base.ctypes.data, base.size,
+                                               off.ctypes.data if off is not None else None,
+                                               length.ctypes.data if length is not None else None,
+                                               stride, flen, n, ok.ctypes.data, ctypes.byref(nbad), pay.ctypes.data)
+    if st not in (VAL_OK, VAL_ERR_CRC):
+        _check(st, "val_crc32_verify_frames_ex_host")
+    return st, ok, int(nbad.value), pay
+
+
+def fold_payload_states(state: int, pay_state, pay_len, ok=None) -> tuple[int, int]:
+    """Receiver rolling CRC over in-order payload states -> (state, frames folded)."""
+    ps = np.ascontiguousarray(pay_state, dtype=np.uint32)
+    pl = np.ascontiguousarray(pay_len, dtype=np.uint32)
+    okk = np.ascontiguousarray(ok, dtype=np.uint8) if ok is not None else None
+    nf = ctypes.c_uint32(0)
+    r = lib().val_crc32_fold_payload_states(state & 0xFFFFFFFF, ps.ctypes.data, pl.ctypes.data,
+                                            okk.ctypes.data if okk is not None else None, ps.size, ctypes.byref(nf))
+    return int(r), int(nf.value)
 
 
 def set_host_chunk_bytes(nbytes: int) -> None:

@@ -55,7 +55,13 @@ struct FrameParams {
     uint32_t *heads;         // ragged mode: 8 work-queue heads, 64 B apart, zero on entry
     uint32_t *bin_counts;    // ragged mode: k_bin_count's bucket totals, re-zeroed here for the next batch
     const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
+    uint32_t *out_pay;       // RX by-product: raw zero-init register of each frame's payload (nullable)
 };
+
+// Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
+// offset when flags (byte 1) has VAL_DATA_OFFSET_PRESENT (reference
+// include/val_wire.h:45, src/val_core.c:743-766).
+__device__ __forceinline__ uint32_t payload_prefix(uint32_t hdr_word0) { return (hdr_word0 & 0x100u) ? 16u : 8u; }
 
 // A full 64-B unit at a dword-aligned address: four dwordx4 loads. Every
 // unit is dword-aligned by construction (hash_frame anchors the unit grid at
@@ -161,7 +167,9 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // pre() runs once this frame's first loads are issued and before the first
 // LDS read: a launch's first call passes the LDS fill and the barrier, so the
 // latency of round 0 runs under them.
-template <int GT, int PF, typename Pre>
+// PAY: also write the payload state (p.out_pay); a separate instantiation so
+// the TX and plain verify kernels carry none of its registers.
+template <int GT, int PF, bool PAY, typename Pre>
 __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre)
 {
@@ -264,13 +272,23 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
     // The tb <= 3 bytes past the grid and, on verify, the stored trailer: all
     // issued before the merge, which hides their round trip (a byte loop after
     // it waited once per byte).
-    uint32_t tail[3] = {0, 0, 0}, trailer = 0;
+    uint32_t tail[3] = {0, 0, 0}, trailer = 0, pw[4] = {0, 0, 0, 0};
     if (active && g == G - 1) {
         if (tb && Lg >= 4) {
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) tail[j] = fp[Lg + min(j, tb - 1)];
         }
         if (p.verify) trailer = ld32(fp + L);
+        // payload by-product: the frame's first 16 bytes (L1/L2 hits: the
+        // unit-0 lane read them in round 0)
+        if (PAY && L >= 8) {
+            pw[0] = ld32(fp);
+            pw[1] = ld32(fp + 4);
+            if (L >= 16) {
+                pw[2] = ld32(fp + 8);
+                pw[3] = ld32(fp + 12);
+            }
+        }
     }
     // Merge: level j joins blocks of 2^j lanes, the left one advanced by 64 * 2^j
     // bytes (LDS nibble map: 8 lookups, where a bit-matrix product costs 96 VALU).
@@ -290,6 +308,20 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
         }
         const uint32_t crc = acc ^ p.xorout;
         if (p.out_crc) p.out_crc[f] = crc;
+        if (PAY) {
+            // RX rolling file CRC by-product (reference src/val_receiver.c:794,
+            // 891): payload register from zero = frame register ^ (register
+            // after the prefix, advanced over the payload's length), by
+            // linearity. Frames shorter than their prefix carry no payload.
+            const uint32_t pre = L >= 8 ? payload_prefix(pw[0]) : 0xFFFFFFFFu;
+            uint32_t pay = 0;
+            if (L >= 8 && L >= pre) {
+                uint32_t h = s4_step(s4_step(seed, pw[0], sb), pw[1], sb);
+                if (pre == 16u) h = s4_step(s4_step(h, pw[2], sb), pw[3], sb);
+                pay = acc ^ shift_bytes(h, L - pre, p.consts);
+            }
+            p.out_pay[f] = pay;
+        }
         if (p.verify) {
             const bool good = (crc == trailer);
             if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
@@ -319,7 +351,7 @@ __device__ uint64_t g_vcrc_time[4096 * 4];
 // the static deal is kept.
 // One frame group of a uniform wave: hash group f.., fetch the next group's
 // descriptors meanwhile, advance.
-template <int G, int PF, typename Pre>
+template <int G, int PF, bool PAY, typename Pre>
 __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
                                            uint64_t step, int lane, const SliceBases &sb, Pre &&pre)
 {
@@ -327,14 +359,14 @@ __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, ui
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    hash_frame<G, PF>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
+    hash_frame<G, PF, PAY>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
     f = fn;
     off = off_n;
     L = L_n;
     fb += step;
 }
 
-template <int G, int PF>
+template <int G, int PF, bool PAY>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
     VCRC_STAMP(0);
@@ -354,12 +386,13 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loads are issued. Peeled, so the LDS image's registers are dead in the
     // loop.
     const LdsImage &cim = im;
-    group_pass<G, PF>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim] {
+    group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &p] {
         lds_tables_write(cim);
+        if (PAY) lds_pow_maps(p.consts);
         __syncthreads();
         VCRC_STAMP(1);
     });
-    while (fb < p.n) group_pass<G, PF>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    while (fb < p.n) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
     VCRC_STAMP(2);
 }
 
@@ -556,7 +589,7 @@ __device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, 
 // static; item i + 2 is dequeued while item i hashes and item i + 1's
 // descriptors load, so neither latency is exposed. All four classes' gap maps
 // stay in LDS: waves never synchronise after the prologue.
-template <int PF>
+template <int PF, bool PAY>
 __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
 {
     VCRC_STAMP(0);
@@ -565,6 +598,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     // order, descriptors), so the LDS fill is not overlapped with them here:
     // its registers would be live through the loop (a spill at 128 VGPRs).
     build_lds_tables(p.consts);
+    if (PAY) lds_pow_maps(p.consts);
     __syncthreads();
     VCRC_STAMP(1);
     const uint32_t *ctab = p.plan;
@@ -597,7 +631,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
         const int G = class_lanes(cur.c);
-        hash_frame<0, PF>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
+        hash_frame<0, PF, PAY>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
         if (it_n >= items) {
             VCRC_STAMP(2);
             break;

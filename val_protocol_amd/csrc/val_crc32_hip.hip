@@ -219,11 +219,15 @@ int prefetch_depth()
 template <int G>
 void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
 {
+    if (p.out_pay) {  // payload states: the default depth only
+        hipLaunchKernelGGL((k_frames<G, 1, true>), grid, dim3(kBlock), 0, s, p);
+        return;
+    }
     switch (pf) {
-    case 0: hipLaunchKernelGGL((k_frames<G, 0>), grid, dim3(kBlock), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((k_frames<G, 2>), grid, dim3(kBlock), 0, s, p); break;
-    case 4: hipLaunchKernelGGL((k_frames<G, 4>), grid, dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_frames<G, 1>), grid, dim3(kBlock), 0, s, p); break;
+    case 0: hipLaunchKernelGGL((k_frames<G, 0, false>), grid, dim3(kBlock), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((k_frames<G, 2, false>), grid, dim3(kBlock), 0, s, p); break;
+    case 4: hipLaunchKernelGGL((k_frames<G, 4, false>), grid, dim3(kBlock), 0, s, p); break;
+    default: hipLaunchKernelGGL((k_frames<G, 1, false>), grid, dim3(kBlock), 0, s, p); break;
     }
 }
 
@@ -278,6 +282,7 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, hipStream_
     if (p.out_crc) t.out_crc = p.out_crc + n_main;
     if (p.out_hdr) t.out_hdr = p.out_hdr + n_main;
     if (p.out_ok) t.out_ok = p.out_ok + n_main;
+    if (p.out_pay) t.out_pay = p.out_pay + n_main;
     val_status_t st = launch_uniform_one(c, m, G, s);
     return st == VAL_OK ? launch_uniform_one(c, t, Gt, s) : st;
 }
@@ -353,8 +358,9 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
         const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
         const unsigned blocks = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>((uint64_t)c.cus, (max_items + kWavesPerBlock - 1) / kWavesPerBlock));
-        if (forced_prefetch() == 0) hipLaunchKernelGGL(k_frames_ragged<0>, dim3(blocks), dim3(kBlock), 0, s, p);
-        else hipLaunchKernelGGL(k_frames_ragged<1>, dim3(blocks), dim3(kBlock), 0, s, p);
+        if (p.out_pay) hipLaunchKernelGGL((k_frames_ragged<1, true>), dim3(blocks), dim3(kBlock), 0, s, p);
+        else if (forced_prefetch() == 0) hipLaunchKernelGGL((k_frames_ragged<0, false>), dim3(blocks), dim3(kBlock), 0, s, p);
+        else hipLaunchKernelGGL((k_frames_ragged<1, false>), dim3(blocks), dim3(kBlock), 0, s, p);
         e = hipGetLastError();
         a.counts_zero = e == hipSuccess;
     }
@@ -656,7 +662,7 @@ uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t l
 constexpr uint64_t kHostZeroCopy = 256u << 10;
 val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_t hi, const uint64_t *off,
                                const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, int verify,
-                               uint32_t hint, uint32_t *crc, uint32_t *hdr, uint8_t *ok, uint32_t *nbad)
+                               uint32_t hint, uint32_t *crc, uint32_t *hdr, uint8_t *ok, uint32_t *nbad, uint32_t *pay)
 {
     const size_t span = (size_t)(hi - lo), desc = off ? (size_t)n * 12u : 0u;
     const size_t span_al = (span + 15u) & ~(size_t)15u;
@@ -664,7 +670,7 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
     val_status_t st;
     if ((st = grow_pinned(&c.h_bounce[0], &c.h_bounce_cap[0], (pinned ? 0u : span_al) + desc + 16u)) != VAL_OK)
         return st;
-    if ((st = grow_pinned(&c.h_out, &c.h_out_cap, (size_t)n * 9u + 16u)) != VAL_OK) return st;
+    if ((st = grow_pinned(&c.h_out, &c.h_out_cap, (size_t)n * 13u + 16u)) != VAL_OK) return st;
     VCRC_HIP(hipEventSynchronize(c.h2d_done[0]), "hipEventSynchronize");  // nothing still reads bounce 0
     uint8_t *b = c.h_bounce[0];
     const uint8_t *frames = base + lo;
@@ -682,7 +688,8 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
     }
     uint32_t *h_crc = reinterpret_cast<uint32_t *>(c.h_out);
     uint32_t *h_hdr = h_crc + n;
-    uint8_t *h_ok = reinterpret_cast<uint8_t *>(h_hdr + n + 4);
+    uint32_t *h_pay = h_hdr + n;
+    uint8_t *h_ok = reinterpret_cast<uint8_t *>(h_pay + n + 4);
     FrameParams p{};
     p.base = frames;
     p.off = h_off;
@@ -698,12 +705,14 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
     p.verify = verify ? 1u : 0u;
     p.out_ok = (ok || nbad) ? h_ok : nullptr;
     p.nbad = nullptr;
+    p.out_pay = pay ? h_pay : nullptr;
     hipStream_t s = c.stream;
     if ((st = launch_frames(c, p, hint, s)) != VAL_OK) return st;
     VCRC_HIP(hipEventRecord(c.h2d_done[0], s), "hipEventRecord");  // the kernel reads bounce 0
     VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
     if (crc) memcpy(crc, h_crc, (size_t)n * 4u);
     if (hdr) memcpy(hdr, h_hdr, (size_t)n * 4u);
+    if (pay) memcpy(pay, h_pay, (size_t)n * 4u);
     if (ok) memcpy(ok, h_ok, n);
     if (nbad) {
         uint32_t bad = 0;
@@ -721,7 +730,7 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
 // non-decreasing (a packed stream); otherwise the whole span is one chunk.
 val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                          uint64_t stride, uint32_t flen, uint32_t n, int verify, uint32_t *crc, uint32_t *hdr,
-                         uint8_t *ok, uint32_t *nbad)
+                         uint8_t *ok, uint32_t *nbad, uint32_t *pay = nullptr)
 {
     if (!base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
     if ((off == nullptr) != (len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
@@ -742,7 +751,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     Ctx &c = *cp;
     std::lock_guard<std::recursive_mutex> lk(c.mu);
     const size_t desc_bytes = off ? (size_t)n * 12u : 0u;
-    const size_t out_bytes = (size_t)n * 9u + 16u;
+    const size_t out_bytes = (size_t)n * 13u + 16u;
     if (n) {
         uint64_t lo = UINT64_MAX, hi = 0;
         for (uint32_t i = 0; i < n; i++) {
@@ -752,7 +761,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         }
         if (hi - lo <= kHostZeroCopy)
             return frames_host_small(c, base, lo, hi, off, len, stride, flen, n, verify, lmin == lmax ? lmax : 0u, crc,
-                                     hdr, ok, nbad);
+                                     hdr, ok, nbad, pay);
     }
     if ((st = grow(&c.d_small, &c.d_small_cap, desc_bytes + out_bytes + 64)) != VAL_OK) return st;
     hipStream_t s = c.stream, cs = c.copy;
@@ -761,7 +770,8 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     uint32_t *d_len = off ? reinterpret_cast<uint32_t *>(sm + (size_t)n * 8u) : nullptr;
     uint32_t *d_crc = reinterpret_cast<uint32_t *>(sm + desc_bytes);
     uint32_t *d_hdr = d_crc + n;
-    uint32_t *d_nbad = d_hdr + n;
+    uint32_t *d_pay = d_hdr + n;
+    uint32_t *d_nbad = d_pay + n;
     uint8_t *d_ok = reinterpret_cast<uint8_t *>(d_nbad + 4);
     if (off && (size_t)n * 12u <= host_chunk_bytes()) {
         // both descriptor arrays through one bounce and one H2D (d_len follows d_off)
@@ -845,19 +855,21 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         p.verify = verify ? 1u : 0u;
         p.out_ok = ok ? d_ok + ch.i0 : nullptr;
         p.nbad = d_nbad;
+        p.out_pay = pay ? d_pay + ch.i0 : nullptr;
         if ((st = launch_frames(c, p, hint, s)) != VAL_OK) return st;
         VCRC_HIP(hipEventRecord(c.kern_done[k], s), "hipEventRecord");
     }
-    // results land in pinned memory (d_crc | d_hdr | d_nbad | d_ok are contiguous), then are copied out
+    // results land in pinned memory (d_crc | d_hdr | d_pay | d_nbad | d_ok are contiguous), then are copied out
     if ((st = grow_pinned(&c.h_out, &c.h_out_cap, out_bytes)) != VAL_OK) return st;
     VCRC_HIP(hipMemcpyAsync(c.h_out, d_crc, out_bytes, hipMemcpyDeviceToHost, s), "D2H results");
     VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize");
     const uint8_t *h = c.h_out;
     if (crc) memcpy(crc, h, (size_t)n * 4u);
     if (hdr) memcpy(hdr, h + (size_t)n * 4u, (size_t)n * 4u);
+    if (pay) memcpy(pay, h + (size_t)n * 8u, (size_t)n * 4u);
     uint32_t bad = 0;
-    memcpy(&bad, h + (size_t)n * 8u, 4);
-    if (ok) memcpy(ok, h + (size_t)n * 8u + 16u, (size_t)n);
+    memcpy(&bad, h + (size_t)n * 12u, 4);
+    if (ok) memcpy(ok, h + (size_t)n * 12u + 16u, (size_t)n);
     if (nbad) *nbad = bad;
     return VAL_OK;
 }
@@ -973,6 +985,43 @@ val_status_t region_host_multi(const void *data, uint64_t len, uint32_t state_in
     }
     *state_out = acc;
     return VAL_OK;
+}
+
+// Rolling file CRC of the RX path from the payload states (reference
+// src/val_receiver.c:794,891: crc_state = val_crc32_update_state(crc_state,
+// payload) per in-order frame): state = shift(state, pay_len) ^ pay_state,
+// frame after frame. x^(8 pay_len) is cached as a nibble map per distinct
+// length, so a window of equal frames costs 8 lookups per frame.
+struct ShiftMap {
+    uint64_t n = UINT64_MAX;
+    uint32_t t[8][16];
+    void set(uint64_t bytes)
+    {
+        if (bytes == n) return;
+        const uint32_t x = gf2_x8n(bytes);
+        for (int k = 0; k < 8; k++)
+            for (int v = 0; v < 16; v++) t[k][v] = gf2_mul(x, (uint32_t)v << (4 * k));
+        n = bytes;
+    }
+    uint32_t apply(uint32_t a) const
+    {
+        uint32_t r = 0;
+        for (int k = 0; k < 8; k++) r ^= t[k][(a >> (4 * k)) & 15u];
+        return r;
+    }
+};
+
+uint32_t fold_payloads(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len, const uint8_t *ok,
+                       uint32_t n, uint32_t *n_folded)
+{
+    ShiftMap m;
+    uint32_t i = 0;
+    for (; i < n && (!ok || ok[i]); i++) {
+        m.set(pay_len[i]);
+        state = m.apply(state) ^ pay_state[i];
+    }
+    if (n_folded) *n_folded = i;
+    return state;
 }
 
 void ctx_free(Ctx &c)
@@ -1278,6 +1327,58 @@ val_status_t val_crc32_verify_frames_host_multi(const uint8_t *base, uint64_t ba
     if (nbad) *nbad = bad;
     if (st == VAL_OK && bad) return VAL_ERR_CRC;
     return st;
+}
+
+val_status_t val_crc32_verify_frames_ex_dev(const uint8_t *d_base, const uint64_t *d_off, const uint32_t *d_len,
+                                            uint64_t stride, uint32_t flen, uint32_t n, uint32_t len_hint,
+                                            uint8_t *d_ok, uint32_t *d_nbad, uint32_t *d_crc, uint32_t *d_hdr,
+                                            uint32_t *d_pay, void *stream)
+{
+    t_err.clear();
+    if ((d_off == nullptr) != (d_len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
+    if (!d_base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
+    Ctx *c = nullptr;
+    val_status_t st = cur(&c);
+    if (st != VAL_OK) return st;
+    FrameParams p{};
+    p.base = d_base;
+    p.off = d_off;
+    p.len = d_len;
+    p.stride = stride;
+    p.flen = flen;
+    p.last_len = flen;
+    p.n = n;
+    p.seed0 = p.seed_rest = 0xFFFFFFFFu;
+    p.xorout = 0xFFFFFFFFu;
+    p.out_crc = d_crc;
+    p.out_hdr = d_hdr;
+    p.verify = 1;
+    p.out_ok = d_ok;
+    p.nbad = d_nbad;
+    p.out_pay = d_pay;
+    return launch_frames(*c, p, d_off ? len_hint : flen, pick_stream(stream));
+}
+
+val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
+                                             const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n,
+                                             uint8_t *ok, uint32_t *nbad, uint32_t *pay)
+{
+    t_err.clear();
+    uint32_t bad = 0;
+    val_status_t st = frames_host(base, base_len, off, len, stride, flen, n, 1, nullptr, nullptr, ok, &bad, pay);
+    if (nbad) *nbad = bad;
+    if (st == VAL_OK && bad) return VAL_ERR_CRC;
+    return st;
+}
+
+uint32_t val_crc32_fold_payload_states(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len,
+                                       const uint8_t *ok, uint32_t n, uint32_t *n_folded)
+{
+    if (!pay_state || !pay_len) {
+        if (n_folded) *n_folded = 0;
+        return state;
+    }
+    return fold_payloads(state, pay_state, pay_len, ok, n, n_folded);
 }
 
 val_status_t val_crc32_region_host_multi(const void *data, uint64_t len, uint32_t state_in, uint32_t *state_out,

@@ -121,3 +121,15 @@ val_status_t val_frame_scan(const uint8_t *stream, size_t len, size_t mtu, uint3
         *consumed = pos;
     return st;
 }
+
+void val_frame_payload_lens(const uint8_t *stream, const uint64_t *frame_off, const uint32_t *crc_len, uint32_t n,
+                            uint32_t *pay_len)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t L = crc_len[i];
+        uint32_t pre = VAL_WIRE_HEADER_SIZE;
+        if (L >= VAL_WIRE_HEADER_SIZE && (stream[frame_off[i] + 1] & VAL_DATA_OFFSET_PRESENT))
+            pre += 8u;
+        pay_len[i] = L >= pre ? L - pre : 0u;
+    }
+}

@@ -77,4 +77,15 @@ def scan_frames(stream: np.ndarray, mtu: int, max_frames: int = 1 << 30):
     return st, frame_off[: nf.value], crc_len[: nf.value], used.value
 
 
-__all__ = ["serialize_header", "deserialize_header", "build_data_batch", "put_trailers", "scan_frames", "ValError"]
+def payload_lens(stream: np.ndarray, frame_off, crc_len) -> np.ndarray:
+    """Payload bytes of each frame (val_frame_payload_lens)."""
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    frame_off = np.ascontiguousarray(frame_off, dtype=np.uint64)
+    crc_len = np.ascontiguousarray(crc_len, dtype=np.uint32)
+    out = np.zeros(crc_len.size, dtype=np.uint32)
+    lib().val_frame_payload_lens(stream.ctypes.data, frame_off.ctypes.data, crc_len.ctypes.data, crc_len.size,
+                                 out.ctypes.data)
+    return out
+
+
+__all__ = ["serialize_header", "deserialize_header", "build_data_batch", "put_trailers", "scan_frames", "payload_lens", "ValError"]
