@@ -74,7 +74,8 @@ def test_regions_host(vc, golden):
 
 # ---- region (device) ---------------------------------------------------------
 @pytest.mark.parametrize("L", [0, 1, 2, 3, 4, 5, 7, 8, 63, 64, 65, 127, 128, 4095, 4096, 4097, 65535, 65536,
-                               65537, 1_000_003, (64 << 20) + 7])
+                               65537, 69632, 69633, 1_000_003, (16 << 20) - 1, 16 << 20, (16 << 20) + 1,
+                               (64 << 20) + 7, 16 * 4096 * 4096 + 4096 * 17 + 3])
 def test_region_dev(vc, dev, L):
     data = _prng.prng_bytes(0xAB00 + L % 977, L)
     d = torch.from_numpy(data).to(dev)
@@ -82,6 +83,43 @@ def test_region_dev(vc, dev, L):
         out = vc.region(d, state_in)
         torch.cuda.synchronize()
         assert int(_u32(out)[0]) == _oracle.update_state(state_in, data)
+
+
+@pytest.mark.parametrize("piece", [65537, 1 << 20, 3 << 20])
+def test_region_chained_pieces(vc, dev, piece, monkeypatch):
+    """Windows longer than one k_region launch covers (2^43 B) are chained
+    pieces, each seeded from the previous result in device memory; the piece
+    size is lowered here so the chaining runs."""
+    import subprocess
+    import sys
+
+    code = f"""
+import sys; sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+import numpy as np, torch
+import val_protocol_amd.crc as vc
+from tests import _oracle, _prng
+vc.init(0)
+data = _prng.prng_bytes(0xC4A1, 10_000_019)
+d = torch.from_numpy(data).to('cuda:0')
+for s in (0xFFFFFFFF, 0x1234ABCD):
+    out = vc.region(d, s)
+    torch.cuda.synchronize()
+    assert (int(out.item()) & 0xFFFFFFFF) == _oracle.update_state(s, data), s
+print('ok')
+"""
+    env = dict(os.environ, VAL_GPU_REGION_MAX_PIECE=str(piece))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def test_region_2gib_window(vc, dev):
+    """W = 512 KiB chunks, 4,096 of them: the full oracle over 2 GiB + 3."""
+    L = (2 << 30) + 3
+    g = torch.Generator(device=dev).manual_seed(0x2618)
+    d = torch.randint(0, 256, (L,), dtype=torch.uint8, device=dev, generator=g)
+    out = vc.region(d, 0x0BADF00D)
+    torch.cuda.synchronize()
+    assert int(_u32(out)[0]) == _oracle.update_state(0x0BADF00D, d.cpu().numpy())
 
 
 def test_region_256mib_window(vc, dev):

@@ -13,9 +13,10 @@
 //                       8 tables x 16 words; a lookup of nibble k reads one of
 //                       16 consecutive words, so lanes either share a word
 //                       (broadcast) or hit distinct banks: no replicas needed.
-//   [134.5 KiB, +8 KiB) 16 nibble maps "advance 2^k bytes", k = 0..15: the
-//                       variable shift of the RX payload-state by-product
-//                       (filled only by launches that ask for it).
+//   [134.5 KiB, +8 KiB) 16 nibble maps "advance 2^(k0+i) bytes", i = 0..15:
+//                       k0 = 0 for the variable shift of the RX payload-state
+//                       by-product, k0 = log2(chunk) for the region fold
+//                       (filled only by launches that use them).
 // T_k[b] = b * x^(8(k+1)) mod P (T_0 = the classic table of the reference,
 // src/val_core.c:133-148).
 #pragma once
@@ -34,7 +35,8 @@ constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kLdsS4 = 0;
 constexpr uint32_t kLdsMaps = 131072;
 constexpr uint32_t kNumMaps = 7 + 6;   // gap maps G = 2^0..2^6, merge maps j = 0..5
-constexpr uint32_t kNumPowMaps = 16;   // "advance 2^k bytes", k = 0..15
+constexpr uint32_t kNumPowMaps = 16;   // LDS slots of "advance 2^(k0+i) bytes"
+constexpr uint32_t kBlobPowMaps = 48;  // blob maps "advance 2^k bytes", k = 0..47
 constexpr uint32_t kLdsPow = kLdsMaps + kNumMaps * 512;
 constexpr uint32_t kLdsWords = (kLdsPow + kNumPowMaps * 512) / 4;
 constexpr int kMaxTree = 6;            // log2(64 lanes)
@@ -110,12 +112,12 @@ __host__ __device__ constexpr uint32_t pow_map(int k) { return kLdsPow + (uint32
 //   [kConstGap,   +7*128)  nibble map "advance (G - 1) * 64 bytes" for G = 2^i,
 //                          entry k * 16 + n = image of n << 4k
 //   [kConstTree,  +6*128)  nibble map "advance 64 * 2^j bytes" (merge level j)
-//   [kConstPow,  +16*128)  nibble map "advance 2^k bytes", k = 0..15
+//   [kConstPow,  +48*128)  nibble map "advance 2^k bytes", k = 0..47
 //   [kConstPowHi,    +16)  x^(8 * 2^k) mod P for k = 16..31 (shifts past 64 KiB, VALU)
 // The maps are contiguous, in LDS order.
 constexpr uint32_t kConstSlice = 0, kConstGap = 1024, kConstTree = 1024 + 7 * 128;
 constexpr uint32_t kConstPow = kConstTree + kMaxTree * 128;
-constexpr uint32_t kConstPowHi = kConstPow + kNumPowMaps * 128;
+constexpr uint32_t kConstPowHi = kConstPow + kBlobPowMaps * 128;
 constexpr uint32_t kConstWords = kConstPowHi + 16;
 
 // Prologue: the slice tables are written in 16-B chunks, chunk c = r * 1024 + t
@@ -175,14 +177,14 @@ __device__ __forceinline__ void build_lds_tables(const uint32_t *consts)
     lds_tables_write(im);
 }
 
-// The 16 "advance 2^k bytes" maps (2 words per thread), for launches that
-// emit payload states; the caller's barrier publishes them.
-__device__ __forceinline__ void lds_pow_maps(const uint32_t *consts)
+// The 16 maps "advance 2^(k0+i) bytes" into the LDS pow slots (2 words per
+// thread); the caller's barrier publishes them.
+__device__ __forceinline__ void lds_pow_maps(const uint32_t *consts, uint32_t k0 = 0)
 {
     constexpr uint32_t kPowWords = kNumPowMaps * 128u;
     uint32_t v[2];
 #pragma unroll
-    for (int r = 0; r < 2; r++) v[r] = consts[kConstPow + (uint32_t)r * kBlock + threadIdx.x];
+    for (int r = 0; r < 2; r++) v[r] = consts[kConstPow + k0 * 128u + (uint32_t)r * kBlock + threadIdx.x];
 #pragma unroll
     for (int r = 0; r < 2; r++) s_lds[kLdsPow / 4u + (uint32_t)r * kBlock + threadIdx.x] = v[r];
     static_assert(kPowWords == 2 * kBlock, "two pow-map words per thread");
@@ -215,7 +217,7 @@ __host__ inline void fill_const_blob(uint32_t *w)
         const uint32_t x = gf2_x8n((uint64_t)kUnit << j);
         for (int t = 0; t < 128; t++) w[kConstTree + j * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
     }
-    for (int k = 0; k < (int)kNumPowMaps; k++) {
+    for (int k = 0; k < (int)kBlobPowMaps; k++) {
         const uint32_t x = gf2_x8n((uint64_t)1 << k);
         for (int t = 0; t < 128; t++) w[kConstPow + k * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
     }

@@ -8,7 +8,8 @@
 //                      first), each length class runs its measured lanes per
 //                      frame; a persistent grid walks the sorted items
 //                      longest first. No host round trip.
-// k_combine            K4 stage 2: fold per-chunk raw states of a long region.
+// k_region             K4: long region CRC in one launch (chunk states folded
+//                      per workgroup, then across workgroups by atomics).
 //
 // Frame algorithm (all GF(2)-linear):
 //   A frame's L bytes of CRC input are cut into 64-B units counted from the
@@ -170,7 +171,7 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // PAY: also write the payload state (p.out_pay); a separate instantiation so
 // the TX and plain verify kernels carry none of its registers.
 template <int GT, int PF, bool PAY, typename Pre>
-__device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
+__device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre)
 {
     constexpr int D = PF > 0 ? PF : 1;
@@ -328,6 +329,7 @@ __device__ __forceinline__ void hash_frame(const FrameParams &p, uint64_t f, boo
             if (!good && p.nbad) atomicAdd(p.nbad, 1u);
         }
     }
+    return acc;  // lane G - 1: the frame's raw register (before xorout)
 }
 
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
@@ -646,59 +648,101 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     }
 }
 
-// ---- region stage 2 -----------------------------------------------------------
-// Fold per-chunk raw states: chunks 0..n-2 are `clen` bytes, chunk n-1 is
-// `last_len`. One workgroup, pairwise GF(2) tree in LDS; level j advances the
-// left state by clen * 2^j bytes with 8 lookups in a nibble map the prologue
-// builds from x^(8 clen 2^j) (one gf2_mul per map entry), the final step by
-// last_len bytes.
-constexpr int kMaxChunks = 8192;
-constexpr int kMaxLevels = 13;  // ceil(log2(kMaxChunks - 1))
-struct CombineParams {
-    const uint32_t *states;
-    uint32_t n;
-    uint32_t *out;
-    uint32_t levels;               // ceil(log2(n-1)) levels of "advance clen * 2^j"
-    uint32_t xlev[kMaxLevels];     // x^(8 clen 2^j) mod P
-    uint32_t xlast;                // x^(8 last_len) mod P
+// ---- K4: region CRC, one launch --------------------------------------------
+// A long window of len bytes is cut into C chunks of W = 2^k0 bytes (k0 >= 12)
+// anchored at the window END: chunk c covers [len - (C-c) W, len - (C-c-1) W),
+// so only chunk 0 can be short. One wave hashes one chunk (hash_frame at 64
+// lanes; chunk 0 carries state_in, the others start from zero), so every
+// combine below advances a left state over whole right subtrees of full
+// chunks, W * 2^j bytes: LDS maps "advance 2^(k0+j) bytes" from the constant
+// blob, nothing built at run time. Chunks are numbered in a padded space of
+// 16 * nwg with the real ones at the end (zero states in front are inert).
+//   workgroup b: its 16 chunk states -> one state S_b (4-level shuffle tree);
+//   S_b advanced over the (nwg - 1 - b) * 16 W bytes after it is atomically
+//   XORed into an accumulator (the fold is linear); the last workgroup to
+//   count in (device-scope atomics, each returned before the next is issued)
+//   takes the accumulator, writes the result and re-zeroes the scratch.
+// Replaces a chunk-state kernel + a single-workgroup combine launch that
+// built its maps with gf2_mul on every call (26 us for an 8 MiB window).
+struct RegionParams {
+    const uint8_t *base;
+    uint64_t len;
+    uint64_t W;               // chunk bytes, 2^k0
+    uint32_t C;               // chunks
+    uint32_t nwg;             // workgroups = ceil(C / 16)
+    uint32_t k0;              // log2(W)
+    uint32_t seed;            // state_in (unless seed_dev)
+    const uint32_t *seed_dev; // state_in read from device memory (chained pieces), nullable
+    uint32_t *out;            // raw register of the window
+    uint32_t *acc;            // scratch: acc[0] accumulator, acc[16] arrival count (zero on entry, re-zeroed)
+    const uint32_t *consts;
 };
+constexpr uint32_t kRegionMaxChunks = 4096;  // nwg <= 256: 8 levels of workgroup fold
 
-__device__ __forceinline__ uint32_t map_apply_at(const uint32_t *map, uint32_t a)
+__global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
 {
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) r ^= map[k * 16 + ((a >> (4 * k)) & 15u)];
-    return r;
-}
-
-__global__ __launch_bounds__(1024) void k_combine(const CombineParams p)
-{
-    __shared__ uint32_t v[kMaxChunks];
-    __shared__ uint32_t maps[(kMaxLevels + 1) * 128];  // level maps, then the last_len map
-    const uint32_t m = p.n - 1;          // equal-length chunks
-    const uint32_t P = 1u << p.levels;   // padded to a power of two, zeros in front
-    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) v[i] = (i >= P - m) ? p.states[i - (P - m)] : 0u;
-    for (uint32_t t = threadIdx.x; t < (p.levels + 1) * 128u; t += blockDim.x) {
-        const uint32_t j = t >> 7, e = t & 127u;
-        const uint32_t x = j < p.levels ? p.xlev[j] : p.xlast;
-        maps[(j < p.levels ? j : (uint32_t)kMaxLevels) * 128u + e] = gf2_mul(x, (e & 15u) << (4u * (e >> 4)));
-    }
+    __shared__ uint32_t s_fold[kWavesPerBlock];
+    LdsImage im;
+    lds_tables_issue(rp.consts, im);
+    const int lane = threadIdx.x & 63, wi = threadIdx.x >> 6;
+    const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
+    const uint32_t pad = rp.nwg * kWavesPerBlock - rp.C;
+    const uint32_t cp = blockIdx.x * kWavesPerBlock + (uint32_t)wi;  // padded chunk index
+    const bool real = cp >= pad;
+    const uint32_t c = real ? cp - pad : 0u;
+    const uint64_t hi = rp.len - (uint64_t)(rp.C - 1u - c) * rp.W;
+    const uint64_t lo = hi > rp.W ? hi - rp.W : 0u;
+    FrameParams p{};
+    p.base = rp.base;
+    p.n = rp.C;
+    p.seed0 = rp.seed_dev ? *rp.seed_dev : rp.seed;
+    p.seed_rest = 0;
+    p.consts = rp.consts;
+    const LdsImage &cim = im;
+    const uint32_t k0 = rp.k0;
+    const uint32_t *consts = rp.consts;
+    const uint32_t st = hash_frame<64, 1, false>(p, c, real, lo, real ? (uint32_t)(hi - lo) : 0u, lane, sb, 64,
+                                                 [&cim, k0, consts] {
+                                                     lds_tables_write(cim);
+#ifndef VCRC_REGION_NOPOW  // diagnostic A/B builds only
+                                                     lds_pow_maps(consts, k0);
+#endif
+                                                     __syncthreads();
+                                                 });
+#ifdef VCRC_REGION_HASHONLY  // diagnostic A/B builds only
+    if (lane == 63 && wi == 0) *rp.out = st;
+    return;
+#endif
+    if (lane == 63) s_fold[wi] = real ? st : 0u;
     __syncthreads();
-    uint32_t width = P;
-    for (uint32_t lv = 0; lv < p.levels; lv++) {
-        const uint32_t half = width >> 1;
-        uint32_t tmp[kMaxChunks / 2 / 1024];
-        int cnt = 0;
-        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) tmp[cnt++] = map_apply_at(maps + lv * 128u, v[2 * i]) ^ v[2 * i + 1];
-        __syncthreads();
-        cnt = 0;
-        for (uint32_t i = threadIdx.x; i < half; i += blockDim.x) v[i] = tmp[cnt++];
-        __syncthreads();
-        width = half;
+    if (wi != 0) return;
+    // 16 chunk states -> S_b: level j advances the left half by W * 2^j
+    uint32_t v = lane < kWavesPerBlock ? s_fold[lane] : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t other = __shfl_xor(v, 1 << j);
+        const bool right = (lane >> j) & 1;
+        const uint32_t left = right ? other : v;
+        v = map_apply(left, pow_map(j)) ^ (right ? v : other);
     }
-    if (threadIdx.x == 0) {
-        const uint32_t head = (m > 0) ? v[0] : 0u;
-        *p.out = map_apply_at(maps + kMaxLevels * 128u, head) ^ p.states[p.n - 1];
+    if (lane != kWavesPerBlock - 1) return;
+    // advance over the (nwg - 1 - b) later workgroups: 16 W * 2^i per set bit i
+    const uint32_t d = rp.nwg - 1u - blockIdx.x;
+    for (int i = 0; i < 12; i++)
+        if ((d >> i) & 1u) v = map_apply(v, pow_map(4 + i));
+#ifdef VCRC_REGION_NOATOMIC  // diagnostic A/B builds only
+    *rp.out = v;
+    return;
+#endif
+    const uint32_t old = atomicXor(&rp.acc[0], v);
+    // the XOR has been performed (its value returned) before this workgroup counts in
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
+    const uint32_t arrived = atomicAdd(&rp.acc[16], 1u);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(arrived) : "memory");
+    if (arrived == rp.nwg - 1u) {
+        const uint32_t total = atomicExch(&rp.acc[0], 0u);
+        atomicExch(&rp.acc[16], 0u);
+        *rp.out = total;
     }
 }
 

@@ -43,7 +43,7 @@ struct Arena {
 // thread, so every entry point sets it before touching HIP.
 struct Ctx {
     std::recursive_mutex mu;
-    Arena region_scratch;         // per-chunk states of a region (<= 32 KiB)
+    Arena region_scratch;         // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin_scratch;            // ragged binning: counts, plan, sorted order
     int device = -1;
     int cus = 0;
@@ -106,10 +106,10 @@ val_status_t ctx_init(Ctx &c, int device)
         VCRC_HIP(hipEventCreateWithFlags(&c.kern_done[i], hipEventDisableTiming), "hipEventCreate");
     }
     {
-        uint32_t blob[kConstWords];
-        fill_const_blob(blob);
-        VCRC_HIP(hipMalloc((void **)&c.d_consts, sizeof blob), "hipMalloc(consts)");
-        VCRC_HIP(hipMemcpy(c.d_consts, blob, sizeof blob, hipMemcpyHostToDevice), "H2D consts");
+        std::vector<uint32_t> blob(kConstWords);
+        fill_const_blob(blob.data());
+        VCRC_HIP(hipMalloc((void **)&c.d_consts, blob.size() * 4u), "hipMalloc(consts)");
+        VCRC_HIP(hipMemcpy(c.d_consts, blob.data(), blob.size() * 4u, hipMemcpyHostToDevice), "H2D consts");
     }
     c.cus = prop.multiProcessorCount;
     return VAL_OK;
@@ -389,34 +389,28 @@ val_status_t launch_frames(Ctx &c, FrameParams &p, uint32_t typical_len, hipStre
 // NULL selects the HIP default (null) stream, as in every HIP API.
 hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 
-// Chunking of a region into "frames" for stage 1: chunks of 2 KiB or more,
-// doubling until there are at most kMaxChunks (8 K) of them. Stage 1 runs
-// them at 32 lanes per chunk, so a large window fills all 4,096 waves (two
-// chunks each: 256 MiB = 8 K chunks of 32 KiB = 16 rounds per lane).
-constexpr uint32_t kRegionLanes = 32;
-constexpr uint64_t kRegionOneFrame = 64u << 10;  // up to 64 KiB: one K1 "frame" at 64 lanes, no combine
-void region_geometry(uint64_t len, uint64_t *clen, uint32_t *nchunks)
+// Region geometry: up to 64 KiB one K1 "frame" at 64 lanes (one launch, no
+// fold); longer windows go to k_region with chunks of W = 2^k0 >= 4 KiB,
+// doubling until there are at most 4,096 chunks (one per wave of the
+// machine; 256 MiB = 4,096 chunks of 64 KiB = 16 rounds per lane).
+constexpr uint64_t kRegionOneFrame = 64u << 10;
+constexpr uint64_t kRegionMaxPiece = (uint64_t)kRegionMaxChunks << 31;  // W <= 2^31: longer windows chain pieces
+void region_geometry(uint64_t len, uint64_t *W, uint32_t *k0, uint32_t *C)
 {
-    if (len <= kRegionOneFrame) {
-        *clen = len ? len : 1;
-        *nchunks = 1;
-        return;
-    }
-    uint64_t c = 2048;
-    while ((len + c - 1) / c > (uint64_t)kMaxChunks) c <<= 1;
-    *clen = c;
-    *nchunks = (uint32_t)(len ? (len + c - 1) / c : 1);
+    uint32_t k = 12;
+    while (((uint64_t)kRegionMaxChunks << k) < len) k++;
+    *k0 = k;
+    *W = (uint64_t)1 << k;
+    *C = (uint32_t)((len + *W - 1) >> k);
 }
 
-val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_out, hipStream_t s)
+val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_out, hipStream_t s,
+                        const uint32_t *seed_dev = nullptr)
 {
-    uint64_t clen;
-    uint32_t n;
-    region_geometry(len, &clen, &n);
-    if (n == 1) {
+    if (len <= kRegionOneFrame && !seed_dev) {
         FrameParams p{};
         p.base = d_ptr;
-        p.stride = clen;
+        p.stride = len ? len : 1;
         p.flen = (uint32_t)len;
         p.last_len = (uint32_t)len;
         p.n = 1;
@@ -425,39 +419,41 @@ val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t sta
         p.out_crc = d_out;
         return launch_frames(c, p, (uint32_t)len, s);
     }
-    std::lock_guard<std::recursive_mutex> lk(c.mu);
-    uint32_t *d_states = nullptr;
-    val_status_t st = arena_acquire(c.region_scratch, (size_t)n * 4u, s, reinterpret_cast<uint8_t **>(&d_states));
-    if (st != VAL_OK) return st;
-    FrameParams p{};
-    p.base = d_ptr;
-    p.stride = clen;
-    p.flen = (uint32_t)clen;
-    p.last_len = (uint32_t)(len - (uint64_t)(n - 1) * clen);
-    p.n = n;
-    p.seed0 = state_in;
-    p.seed_rest = 0;
-    p.xorout = 0;
-    p.out_crc = d_states;
-    st = launch_uniform(c, p, forced_lanes() ? forced_lanes() : kRegionLanes, s);
-    if (st != VAL_OK) {
-        (void)arena_release(c.region_scratch, s);
+    // Beyond 2^43 bytes: pieces chained through the device state (each piece
+    // reads the previous one's result as its seed). VAL_GPU_REGION_MAX_PIECE
+    // lowers the piece size (tests exercise the chaining).
+    static const uint64_t env_piece = getenv("VAL_GPU_REGION_MAX_PIECE") ? strtoull(getenv("VAL_GPU_REGION_MAX_PIECE"), nullptr, 0) : 0;
+    const uint64_t piece = env_piece > kRegionOneFrame ? std::min(env_piece, kRegionMaxPiece) : kRegionMaxPiece;
+    if (len > piece) {
+        val_status_t st = VAL_OK;
+        for (uint64_t o = 0; o < len && st == VAL_OK; o += piece)
+            st = region_dev(c, d_ptr + o, std::min(piece, len - o), state_in, d_out, s, o ? d_out : seed_dev);
         return st;
     }
-    CombineParams cp{};
-    cp.states = d_states;
-    cp.n = n;
-    cp.out = d_out;
-    uint32_t m = n - 1, levels = 0;
-    while ((1u << levels) < m) levels++;
-    cp.levels = levels;
-    uint32_t x = gf2_x8n(clen);
-    for (uint32_t j = 0; j < levels; j++, x = gf2_mul(x, x)) cp.xlev[j] = x;
-    cp.xlast = gf2_x8n(p.last_len);
-    hipLaunchKernelGGL(k_combine, dim3(1), dim3(1024), 0, s, cp);
-    hipError_t e = hipGetLastError();
-    st = arena_release(c.region_scratch, s);
-    if (e != hipSuccess) return fail(VAL_ERR_IO, "k_combine launch", e);
+    std::lock_guard<std::recursive_mutex> lk(c.mu);
+    Arena &a = c.region_scratch;
+    uint8_t *scratch = nullptr;
+    val_status_t st = arena_acquire(a, 128, s, &scratch);
+    if (st != VAL_OK) return st;
+    hipError_t e = a.counts_zero ? hipSuccess : hipMemsetAsync(scratch, 0, 128, s);
+    a.counts_zero = false;
+    if (e == hipSuccess) {
+        RegionParams rp{};
+        rp.base = d_ptr;
+        rp.len = len;
+        region_geometry(len, &rp.W, &rp.k0, &rp.C);
+        rp.nwg = (rp.C + kWavesPerBlock - 1) / kWavesPerBlock;
+        rp.seed = state_in;
+        rp.seed_dev = seed_dev;
+        rp.out = d_out;
+        rp.acc = reinterpret_cast<uint32_t *>(scratch);
+        rp.consts = c.d_consts;
+        hipLaunchKernelGGL(k_region, dim3(rp.nwg), dim3(kBlock), 0, s, rp);
+        e = hipGetLastError();
+        a.counts_zero = e == hipSuccess;  // the last workgroup re-zeroes the scratch
+    }
+    st = arena_release(a, s);
+    if (e != hipSuccess) return fail(VAL_ERR_IO, "k_region launch", e);
     return st;
 }
 
@@ -1282,13 +1278,7 @@ val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t s
     return region_dev(*c, d_ptr, len, state_in, d_state_out, pick_stream(stream));
 }
 
-uint64_t val_crc32_region_scratch_bytes(uint64_t len)
-{
-    uint64_t clen;
-    uint32_t n;
-    region_geometry(len, &clen, &n);
-    return n > 1 ? (uint64_t)n * 4u : 0u;
-}
+uint64_t val_crc32_region_scratch_bytes(uint64_t len) { return len > kRegionOneFrame ? 128u : 0u; }
 
 val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                                    uint64_t stride, uint32_t flen, uint32_t n, uint32_t *crc, uint32_t *hdr)
