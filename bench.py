@@ -103,36 +103,69 @@ def make_ragged_frames(torch, dev, n, seed):
     return buf, d_off, torch.from_numpy(crc_len.astype(np.int32)).to(dev)
 
 
-def cpu_baseline(sample: np.ndarray, stride: int, flen: int, n: int, threads: int):
-    """Time the reference's own val_crc32 (oracle/_ref, built from
-    /root/reference/src) -- or the oracle port if that build is absent --
-    over a host copy of `n` frames of the same workload."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(sample: np.ndarray, n: int, threads: int, stride: int = 0, flen: int = 0, off=None, length=None):
+    """Time the reference's own val_crc32 (oracle/_ref/libref_bench.so, built
+    from /root/reference/src/val_core.c:150-160) -- or the oracle port if that
+    build is absent -- over a host copy of `n` frames of the same workload:
+    once on 1 thread and once on `threads` threads (frames round-robin).
+    Returns (GiB/s at `threads`, GiB/s on 1 thread, kind, outputs, detail)."""
     kind = "reference"
     so = os.path.join(ROOT, "oracle", "_ref", "libref_bench.so")
     out = np.zeros(n, np.uint32)
+    vp, u64, u32, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    if off is not None:
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint32)
+        nbytes = int(length.astype(np.int64).sum())
+    else:
+        nbytes = n * flen
     if os.path.exists(so):
         lib = ctypes.CDLL(so)
-        fn = lib.ref_bench_frames
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
-                       ctypes.c_int]
-        run = lambda: fn(sample.ctypes.data, stride, flen, n, out.ctypes.data, threads)  # noqa: E731
+        if off is not None:
+            fn = lib.ref_bench_frames_desc
+            fn.argtypes = [vp, vp, vp, u64, vp, ci]
+            run = lambda t: fn(sample.ctypes.data, off.ctypes.data, length.ctypes.data, n, out.ctypes.data, t)  # noqa: E731
+        else:
+            fn = lib.ref_bench_frames
+            fn.argtypes = [vp, u64, u32, u64, vp, ci]
+            run = lambda t: fn(sample.ctypes.data, stride, flen, n, out.ctypes.data, t)  # noqa: E731
     else:
         kind = "port"
         from tests import _oracle
 
-        run = lambda: _oracle.lib().oracle_crc32_frames_strided(sample.ctypes.data, stride, flen, n,  # noqa: E731
-                                                                out.ctypes.data, None, threads)
-    run()  # warm caches/pages
-    reps, t_total = 0, 0.0
-    while True:  # accumulate >= ~10 s of CPU (thread) time, <= ~4 s wall
-        t0 = time.perf_counter()
-        run()
-        t_total += time.perf_counter() - t0
-        reps += 1
-        if t_total * threads >= 10.0 or t_total >= 4.0:
-            break
-    gibs = reps * n * flen / t_total / GIB
-    return gibs, kind, out, reps, t_total
+        if off is not None:
+            run = lambda t: _oracle.lib().oracle_crc32_frames(sample.ctypes.data, off.ctypes.data,  # noqa: E731
+                                                              length.ctypes.data, n, out.ctypes.data, None, t)
+        else:
+            run = lambda t: _oracle.lib().oracle_crc32_frames_strided(sample.ctypes.data, stride, flen, n,  # noqa: E731
+                                                                      out.ctypes.data, None, t)
+
+    def rate(t, cpu_s, wall_s):
+        run(t)  # warm caches/pages
+        reps, tt = 0, 0.0
+        while True:  # >= cpu_s of CPU (thread) time or >= wall_s of wall time
+            t0 = time.perf_counter()
+            run(t)
+            tt += time.perf_counter() - t0
+            reps += 1
+            if tt * t >= cpu_s or tt >= wall_s:
+                break
+        return reps * nbytes / tt / GIB, reps
+
+    one, reps1 = rate(1, 3.0, 3.0)
+    many, reps = rate(threads, 10.0, 4.0)
+    return many, one, kind, out, f"x{reps} reps on {threads} threads, x{reps1} on 1 thread"
 
 
 def read_pmc_traffic(config: str):
@@ -301,16 +334,33 @@ def main():
                             "crc_ok": got == _oracle.crc32(win.cpu().numpy())})
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not ragged:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        ns = min(n, max(1, (1 << 30) // flen))  # ~1 GiB host sample of the same frames
-        host_rows = buf[:ns].cpu().numpy().reshape(-1)
-        cgibs, kind, cout, reps, tt = cpu_baseline(host_rows, stride, flen, ns, threads)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.sort_frames:
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            avail = os.cpu_count() or 1
+        threads = args.cpu_threads or min(16, avail)  # the GPU box's CPU share is 16 per GPU
+        if ragged:
+            offs_all = d_off.cpu().numpy()
+            lens_all = d_len.cpu().numpy().astype(np.uint32)
+            ends = offs_all + lens_all.astype(np.int64)
+            ns = int(np.searchsorted(ends, 1 << 30, side="right"))  # ~1 GiB of the batch
+            ns = max(1, min(ns, n))
+            host_rows = flat[: int(ends[ns - 1])].cpu().numpy()
+            cgibs, one, kind, cout, detail = cpu_baseline(host_rows, ns, threads, off=offs_all[:ns],
+                                                          length=lens_all[:ns])
+            sample_bytes = int(lens_all[:ns].astype(np.int64).sum())
+        else:
+            ns = min(n, max(1, (1 << 30) // flen))  # ~1 GiB host sample of the same frames
+            host_rows = buf[:ns].cpu().numpy().reshape(-1)
+            cgibs, one, kind, cout, detail = cpu_baseline(host_rows, ns, threads, stride=stride, flen=flen)
+            sample_bytes = ns * flen
         same = bool(np.array_equal(cout, crc[:ns].cpu().numpy().view(np.uint32))) if not args.verify else None
         cpu = {"value": round(cgibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-               "sample": f"first {ns} frames of this batch ({ns * flen / GIB:.2f} GiB) x{reps} reps, "
-                         f"reference val_crc32 per frame, frames round-robin over {threads} pthreads; "
-                         f"outputs equal GPU: {same}"}
+               "value_1core": round(one, 3), "cpu_model": cpu_model(), "cores_visible": avail,
+               "sample": f"first {ns} frames of this batch ({sample_bytes / GIB:.2f} GiB of CRC input), "
+                         f"reference val_crc32 per frame (src/val_core.c:150-160), frames round-robin over "
+                         f"pthreads, {detail}; outputs equal GPU: {same}"}
 
     if rank == 0:
         metric = "GiB/s device-resident trailer CRC-32 over batched DATA packets, 1 MI355X"

@@ -178,16 +178,28 @@ __device__ __forceinline__ void build_lds_tables(const uint32_t *consts)
 }
 
 // The 16 maps "advance 2^(k0+i) bytes" into the LDS pow slots (2 words per
-// thread); the caller's barrier publishes them.
+// thread), in two halves like the tables: issue the loads early (before any
+// frame load, so waiting for them never waits for frame data), write them in
+// the prologue; the caller's barrier publishes them.
+struct PowImage {
+    uint32_t v[2];
+};
+__device__ __forceinline__ void lds_pow_issue(const uint32_t *consts, uint32_t k0, PowImage &im)
+{
+    static_assert(kNumPowMaps * 128u == 2 * kBlock, "two pow-map words per thread");
+#pragma unroll
+    for (int r = 0; r < 2; r++) im.v[r] = consts[kConstPow + k0 * 128u + (uint32_t)r * kBlock + threadIdx.x];
+}
+__device__ __forceinline__ void lds_pow_write(const PowImage &im)
+{
+#pragma unroll
+    for (int r = 0; r < 2; r++) s_lds[kLdsPow / 4u + (uint32_t)r * kBlock + threadIdx.x] = im.v[r];
+}
 __device__ __forceinline__ void lds_pow_maps(const uint32_t *consts, uint32_t k0 = 0)
 {
-    constexpr uint32_t kPowWords = kNumPowMaps * 128u;
-    uint32_t v[2];
-#pragma unroll
-    for (int r = 0; r < 2; r++) v[r] = consts[kConstPow + k0 * 128u + (uint32_t)r * kBlock + threadIdx.x];
-#pragma unroll
-    for (int r = 0; r < 2; r++) s_lds[kLdsPow / 4u + (uint32_t)r * kBlock + threadIdx.x] = v[r];
-    static_assert(kPowWords == 2 * kBlock, "two pow-map words per thread");
+    PowImage im;
+    lds_pow_issue(consts, k0, im);
+    lds_pow_write(im);
 }
 
 // Advance raw register v over n zero bytes: one LDS nibble map (8 lookups) per

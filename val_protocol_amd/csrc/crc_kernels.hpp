@@ -374,6 +374,8 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     VCRC_STAMP(0);
     LdsImage im;
     lds_tables_issue(p.consts, im);
+    PowImage pim;
+    if (PAY) lds_pow_issue(p.consts, 0, pim);
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
@@ -388,9 +390,10 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loads are issued. Peeled, so the LDS image's registers are dead in the
     // loop.
     const LdsImage &cim = im;
-    group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &p] {
+    const PowImage &cpim = pim;
+    group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
         lds_tables_write(cim);
-        if (PAY) lds_pow_maps(p.consts);
+        if (PAY) lds_pow_write(cpim);
         __syncthreads();
         VCRC_STAMP(1);
     });
@@ -682,8 +685,11 @@ constexpr uint32_t kRegionMaxChunks = 4096;  // nwg <= 256: 8 levels of workgrou
 __global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
 {
     __shared__ uint32_t s_fold[kWavesPerBlock];
+    VCRC_STAMP(0);
     LdsImage im;
     lds_tables_issue(rp.consts, im);
+    PowImage pim;
+    lds_pow_issue(rp.consts, rp.k0, pim);
     const int lane = threadIdx.x & 63, wi = threadIdx.x >> 6;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
     const uint32_t pad = rp.nwg * kWavesPerBlock - rp.C;
@@ -699,16 +705,15 @@ __global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
     p.seed_rest = 0;
     p.consts = rp.consts;
     const LdsImage &cim = im;
-    const uint32_t k0 = rp.k0;
-    const uint32_t *consts = rp.consts;
+    const PowImage &cpim = pim;
     const uint32_t st = hash_frame<64, 1, false>(p, c, real, lo, real ? (uint32_t)(hi - lo) : 0u, lane, sb, 64,
-                                                 [&cim, k0, consts] {
+                                                 [&cim, &cpim] {
                                                      lds_tables_write(cim);
-#ifndef VCRC_REGION_NOPOW  // diagnostic A/B builds only
-                                                     lds_pow_maps(consts, k0);
-#endif
+                                                     lds_pow_write(cpim);
                                                      __syncthreads();
+                                                     VCRC_STAMP(1);
                                                  });
+    VCRC_STAMP(2);
 #ifdef VCRC_REGION_HASHONLY  // diagnostic A/B builds only
     if (lane == 63 && wi == 0) *rp.out = st;
     return;
@@ -739,6 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
     const uint32_t arrived = atomicAdd(&rp.acc[16], 1u);
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(arrived) : "memory");
+    VCRC_STAMP(3);
     if (arrived == rp.nwg - 1u) {
         const uint32_t total = atomicExch(&rp.acc[0], 0u);
         atomicExch(&rp.acc[16], 0u);

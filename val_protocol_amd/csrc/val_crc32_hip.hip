@@ -25,15 +25,22 @@ namespace vcrc {
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-// Device scratch owned by the context and shared by calls on any stream: the
-// caller's stream waits for the previous user's last kernel (an event), so
-// concurrent calls serialise on it instead of allocating per call. Callers
-// hold Ctx::mu from acquire through release.
+// Device scratch of one stream (k_region's accumulator, ragged binning): a
+// stream's calls are ordered by the stream itself, so scratch kept per stream
+// handle needs no events (an event record + wait per call cost ~2.8 us of GPU
+// time on 1 MiB windows, tools/ab_region.py). A destroyed stream's handle is
+// only reused once its work is done, so inheriting its scratch is safe.
+// Callers hold Ctx::mu from acquire through launch.
 struct Arena {
     uint8_t *d = nullptr;
     size_t cap = 0;
-    hipEvent_t last = nullptr;
-    bool counts_zero = false;  // bin scratch: bucket totals known to be zero (launch_ragged)
+    bool counts_zero = false;  // counters known to be zero (k_region, launch_ragged re-zero them)
+};
+
+struct StreamScratch {
+    hipStream_t stream;
+    Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
+    Arena bin;     // ragged binning: counts, plan, sorted order
 };
 
 // One context per HIP device: streams, constant blob, staging and scratch.
@@ -43,8 +50,7 @@ struct Arena {
 // thread, so every entry point sets it before touching HIP.
 struct Ctx {
     std::recursive_mutex mu;
-    Arena region_scratch;         // k_region accumulator + arrival count (128 B, zero between calls)
-    Arena bin_scratch;            // ragged binning: counts, plan, sorted order
+    std::vector<StreamScratch *> scratch;  // per stream handle
     int device = -1;
     int cus = 0;
     hipStream_t stream = nullptr;
@@ -289,11 +295,20 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, hipStream_
 
 // Ragged descriptor batch: counting-sort by length on the device, then one
 // grouped launch planned by bytes per length class (no host synchronisation).
+StreamScratch &scratch_for(Ctx &c, hipStream_t s)
+{
+    for (StreamScratch *x : c.scratch)
+        if (x->stream == s) return *x;
+    c.scratch.push_back(new StreamScratch{s, {}, {}});
+    return *c.scratch.back();
+}
+
+// Scratch of at least `bytes` for stream s. Growing waits for the stream's
+// earlier kernels, which may still use the old block.
 val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out)
 {
-    if (!a.last) VCRC_HIP(hipEventCreateWithFlags(&a.last, hipEventDisableTiming), "hipEventCreate(arena)");
     if (a.cap < bytes) {
-        VCRC_HIP(hipEventSynchronize(a.last), "hipEventSynchronize(arena)");  // earlier users are done
+        VCRC_HIP(hipStreamSynchronize(s), "hipStreamSynchronize(scratch)");
         if (a.d) (void)hipFree(a.d);
         a.d = nullptr;
         a.cap = 0;
@@ -303,22 +318,13 @@ val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out)
         if (e != hipSuccess) return fail(VAL_ERR_NO_MEMORY, "hipMalloc(scratch)", e);
         a.cap = sz;
     }
-    VCRC_HIP(hipStreamWaitEvent(s, a.last, 0), "hipStreamWaitEvent(arena)");
     *out = a.d;
-    return VAL_OK;
-}
-
-val_status_t arena_release(Arena &a, hipStream_t s)
-{
-    VCRC_HIP(hipEventRecord(a.last, s), "hipEventRecord(arena)");
     return VAL_OK;
 }
 
 void arena_free(Arena &a)
 {
-    if (a.last) (void)hipEventSynchronize(a.last);
     if (a.d) (void)hipFree(a.d);
-    if (a.last) (void)hipEventDestroy(a.last);
     a = Arena{};
 }
 
@@ -333,7 +339,7 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
     const size_t sz_heads = 8u * 64u, sz_gcount = (size_t)kBuckets * 4u;
     const size_t total = sz_heads + sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     std::lock_guard<std::recursive_mutex> lk(c.mu);
-    Arena &a = c.bin_scratch;
+    Arena &a = scratch_for(c, s).bin;
     uint8_t *scratch = nullptr;
     val_status_t st = arena_acquire(a, total, s, &scratch);
     if (st != VAL_OK) return st;
@@ -364,9 +370,8 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
         e = hipGetLastError();
         a.counts_zero = e == hipSuccess;
     }
-    st = arena_release(a, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
-    return st;
+    return VAL_OK;
 }
 
 // typical_len == 0 with descriptors means "lengths unknown or mixed": bin them,
@@ -431,7 +436,7 @@ val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t sta
         return st;
     }
     std::lock_guard<std::recursive_mutex> lk(c.mu);
-    Arena &a = c.region_scratch;
+    Arena &a = scratch_for(c, s).region;
     uint8_t *scratch = nullptr;
     val_status_t st = arena_acquire(a, 128, s, &scratch);
     if (st != VAL_OK) return st;
@@ -452,9 +457,8 @@ val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t sta
         e = hipGetLastError();
         a.counts_zero = e == hipSuccess;  // the last workgroup re-zeroes the scratch
     }
-    st = arena_release(a, s);
     if (e != hipSuccess) return fail(VAL_ERR_IO, "k_region launch", e);
-    return st;
+    return VAL_OK;
 }
 
 val_status_t grow(uint8_t **buf, size_t *cap, size_t need)
@@ -1034,8 +1038,13 @@ void ctx_free(Ctx &c)
         if (c.h2d_done[k]) (void)hipEventDestroy(c.h2d_done[k]);
         if (c.kern_done[k]) (void)hipEventDestroy(c.kern_done[k]);
     }
-    arena_free(c.region_scratch);
-    arena_free(c.bin_scratch);
+    (void)hipDeviceSynchronize();  // the streams that used the scratch may be gone
+    for (StreamScratch *x : c.scratch) {
+        arena_free(x->region);
+        arena_free(x->bin);
+        delete x;
+    }
+    c.scratch.clear();
     if (c.h_out) (void)hipHostFree(c.h_out);
     if (c.copy) (void)hipStreamDestroy(c.copy);
     if (c.stream) (void)hipStreamDestroy(c.stream);
