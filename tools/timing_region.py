@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave timeline of one k_region launch from a -DVCRC_TIMING build:
-stamps 0 start, 1 after the LDS prologue, 2 after the chunk hash, 3 after the
-workgroup's atomics (wave 0 only). usage: timing_region.py LIB BYTES..."""
+stamps 0 start, 1 frame loads issued (prologue writes begin), 2 after the
+prologue barrier, 3 after the chunk hash. usage: timing_region.py LIB BYTES..."""
 import ctypes
 import os
 import sys
@@ -37,8 +37,5 @@ for size in [int(x) for x in sys.argv[2:]]:
     us = (t - t0) / 100.0
     pct = lambda a: " ".join(f"{np.percentile(a, q):6.2f}" for q in (0, 50, 100))
     print(f"region {size} B: waves stamped {nw}")
-    for k, name in enumerate(("start", "prologue", "hashed")):
+    for k, name in enumerate(("start", "issued", "barrier", "hashed")):
         print(f"  {name:9s}", pct(us[used, k]))
-    w0 = np.nonzero(used)[0]
-    w0 = w0[w0 % 16 == 0]
-    print("  atomics  ", pct(us[w0, 3]), " (wave 0 of each block)")

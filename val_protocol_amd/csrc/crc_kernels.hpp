@@ -93,11 +93,22 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
 // floor4(frame end)). Unit 0 starts pad bytes before the frame: a word of it
 // wholly before the frame reads the frame's first dword, base + (pad & ~3),
 // instead (no byte outside that dword is touched) and is masked to zero.
-__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad)
+// The loads are issued by every lane, branch-free: a lane without a unit
+// reads 64 B of `dummy` (the constant blob, an L1/L2 hit) instead. Behind a
+// skippable branch, the waitcnt pass could not count them, and the prologue's
+// waits for the constant-blob loads (issued first) then also waited for most
+// of the frame loads: the LDS fill stopped overlapping the first memory
+// latency (region launches: prologue 7.7 us; tools/timing_region.py).
+// BF (k_region): branch-free, every lane issues the loads.
+// Otherwise (k_frames): only lanes with a unit issue them; measured faster on
+// frame batches (the dummy loads cost cfg2 3%, a 256-frame window 9%).
+template <bool BF>
+__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad, gu8 *dummy)
 {
-    if (u >= 0 && Lg >= 4) {
-        gu8 *base = fp + ((int64_t)u * kUnit - pad);
-        const uint32_t lo = u == 0 ? (pad & ~3u) : 0u;
+    const bool has = u >= 0 && Lg >= 4;
+    if (BF || has) {
+        gu8 *base = has ? fp + ((int64_t)u * kUnit - pad) : dummy;
+        const uint32_t lo = (has && u == 0) ? (pad & ~3u) : 0u;
 #pragma unroll
         for (int i = 0; i < kWords; i++) w[i] = *reinterpret_cast<gu32 *>(base + max(4u * (uint32_t)i, lo));
     }
@@ -170,7 +181,8 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // latency of round 0 runs under them.
 // PAY: also write the payload state (p.out_pay); a separate instantiation so
 // the TX and plain verify kernels carry none of its registers.
-template <int GT, int PF, bool PAY, typename Pre>
+// BF: branch-free round-0 loads (load_unit0); k_region only.
+template <int GT, int PF, bool PAY, bool BF, typename Pre>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre)
 {
@@ -194,21 +206,23 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     // order, so hashing it never waits for them.
     uint32_t w0[kWords];
     const bool tiny = u0 == 0 && Lg < 4;
-    load_unit0(w0, u0, fp, Lg, pad);
+    gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
+    load_unit0<BF>(w0, u0, fp, Lg, pad, dummy);
     // header_crc: by the lane holding unit 0, from the frame's first line,
     // which round 0 reads anyway (read after the merge, the line had left the
     // caches: +0.4% HBM traffic on cfg3).
     const bool hdr = R > 0 && u0 == 0 && p.out_hdr;
     uint32_t h0, h1;
-    if (hdr && L >= 8) {
-        h0 = ld32(fp);
-        h1 = ld32(fp + 4);
+    if (BF || (hdr && L >= 8)) {
+        gu8 *hp = (hdr && L >= 8) ? fp : dummy;
+        h0 = ld32(hp);
+        h1 = ld32(hp + 4);
     }
     uint32_t nxt[D][kWords];
     if (PF > 0) {
 #pragma unroll
         for (int d = 0; d < D; d++)
-            if (R > 1u + d) load_full(nxt[d], up + d * kStep);
+            if (BF || R > 1u + d) load_full(nxt[d], R > 1u + d ? up + d * kStep : dummy);
     }
     uint32_t acc = 0;
     // Round 0's leading zero words (unit 0's front padding, lanes without a
@@ -361,7 +375,7 @@ __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, ui
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    hash_frame<G, PF, PAY>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
+    hash_frame<G, PF, PAY, false>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
     f = fn;
     off = off_n;
     L = L_n;
@@ -372,16 +386,19 @@ template <int G, int PF, bool PAY>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
     VCRC_STAMP(0);
-    LdsImage im;
-    lds_tables_issue(p.consts, im);
-    PowImage pim;
-    if (PAY) lds_pow_issue(p.consts, 0, pim);
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
     const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
+    LdsImage im;
+    lds_tables_issue(p.consts, im);
+    PowImage pim;
+    if (PAY) lds_pow_issue(p.consts, 0, pim);
     // Descriptors of the next frame group are fetched while this one hashes.
+    // (Loading the first group's descriptors branch-free before the blob, so
+    // the prologue overlaps the first frame loads exactly, measured slower:
+    // cfg2 -3%, 256-frame windows -9%, cfg3 -1%.)
     uint64_t fb = wave * kGroups, f = fb + (uint64_t)(lane / G), off = 0;
     uint32_t L = 0;
     if (f < p.n) frame_desc(p, f, off, L);
@@ -636,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
         const int G = class_lanes(cur.c);
-        hash_frame<0, PF, PAY>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
+        hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
         if (it_n >= items) {
             VCRC_STAMP(2);
             break;
@@ -706,14 +723,15 @@ __global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
     p.consts = rp.consts;
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
-    const uint32_t st = hash_frame<64, 1, false>(p, c, real, lo, real ? (uint32_t)(hi - lo) : 0u, lane, sb, 64,
+    const uint32_t st = hash_frame<64, 1, false, true>(p, c, real, lo, real ? (uint32_t)(hi - lo) : 0u, lane, sb, 64,
                                                  [&cim, &cpim] {
+                                                     VCRC_STAMP(1);
                                                      lds_tables_write(cim);
                                                      lds_pow_write(cpim);
                                                      __syncthreads();
-                                                     VCRC_STAMP(1);
+                                                     VCRC_STAMP(2);
                                                  });
-    VCRC_STAMP(2);
+    VCRC_STAMP(3);
 #ifdef VCRC_REGION_HASHONLY  // diagnostic A/B builds only
     if (lane == 63 && wi == 0) *rp.out = st;
     return;
@@ -744,7 +762,6 @@ __global__ __launch_bounds__(kBlock) void k_region(const RegionParams rp)
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
     const uint32_t arrived = atomicAdd(&rp.acc[16], 1u);
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(arrived) : "memory");
-    VCRC_STAMP(3);
     if (arrived == rp.nwg - 1u) {
         const uint32_t total = atomicExch(&rp.acc[0], 0u);
         atomicExch(&rp.acc[16], 0u);

@@ -74,7 +74,7 @@ struct Ctx {
 
 constexpr int kMaxDevices = 64;
 std::mutex g_ctx_mu;                     // guards g_ctxs creation / teardown
-Ctx *g_ctxs[kMaxDevices] = {};
+std::atomic<Ctx *> g_ctxs[kMaxDevices] = {};  // published once initialised
 std::atomic<int> g_default_dev{-1};      // first device initialised in this process
 thread_local int t_dev = -1;             // device the calling thread is bound to
 thread_local std::string t_err;
@@ -124,13 +124,20 @@ val_status_t ctx_init(Ctx &c, int device)
 // Context of `device`, created on first use.
 val_status_t get_ctx(int device, Ctx **out)
 {
+    if (device >= 0 && device < kMaxDevices) {  // fast path: no HIP call once initialised
+        Ctx *c = g_ctxs[device].load(std::memory_order_acquire);
+        if (c) {
+            *out = c;
+            return VAL_OK;
+        }
+    }
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count <= 0) return fail(VAL_ERR_IO, "val_gpu_init: no HIP device", e);
     if (device < 0 || device >= count || device >= kMaxDevices)
         return fail(VAL_ERR_INVALID_ARG, "val_gpu_init: device index out of range");
     std::lock_guard<std::mutex> lk(g_ctx_mu);
-    if (!g_ctxs[device]) {
+    if (!g_ctxs[device].load(std::memory_order_acquire)) {
         Ctx *c = new Ctx;
         val_status_t st = ctx_init(*c, device);
         if (st != VAL_OK) {
@@ -138,11 +145,11 @@ val_status_t get_ctx(int device, Ctx **out)
             delete c;
             return st;
         }
-        g_ctxs[device] = c;
+        g_ctxs[device].store(c, std::memory_order_release);
         int none = -1;
         g_default_dev.compare_exchange_strong(none, device);
     }
-    *out = g_ctxs[device];
+    *out = g_ctxs[device].load(std::memory_order_acquire);
     return VAL_OK;
 }
 
@@ -398,7 +405,7 @@ hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 // fold); longer windows go to k_region with chunks of W = 2^k0 >= 4 KiB,
 // doubling until there are at most 4,096 chunks (one per wave of the
 // machine; 256 MiB = 4,096 chunks of 64 KiB = 16 rounds per lane).
-constexpr uint64_t kRegionOneFrame = 64u << 10;
+constexpr uint64_t kRegionOneFrame = 16u << 10;  // one 64-lane frame of <= 4 rounds; k_region is faster above (tools/region_latency.py: 32 KiB 12.1 us as one frame, 10.1 us in k_region)
 constexpr uint64_t kRegionMaxPiece = (uint64_t)kRegionMaxChunks << 31;  // W <= 2^31: longer windows chain pieces
 void region_geometry(uint64_t len, uint64_t *W, uint32_t *k0, uint32_t *C)
 {
@@ -1105,13 +1112,13 @@ void val_gpu_shutdown(void)
 {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     for (int d = 0; d < kMaxDevices; d++) {
-        if (!g_ctxs[d]) continue;
+        Ctx *c = g_ctxs[d].exchange(nullptr);
+        if (!c) continue;
         {
-            std::lock_guard<std::recursive_mutex> lk2(g_ctxs[d]->mu);
-            ctx_free(*g_ctxs[d]);
+            std::lock_guard<std::recursive_mutex> lk2(c->mu);
+            ctx_free(*c);
         }
-        delete g_ctxs[d];
-        g_ctxs[d] = nullptr;
+        delete c;
     }
     g_default_dev.store(-1);
     t_dev = -1;
