@@ -35,6 +35,7 @@ CONFIGS = {
     "cfg5": (262144, 0, True, True),
 }
 CFG5_MIN, CFG5_MAX = 512, 65516  # payload bytes, log-uniform (BASELINE configs[4])
+CFG4_FILE = 8 << 30  # cfg4: one 8 GiB file at MTU 65,536 -> 131,112 x 65,516 B + a last frame of 800 B
 
 
 def parse():
@@ -229,15 +230,26 @@ def main():
         buf, flen, stride = make_frames(torch, dev, n, payload, explicit, first, seed=1234 + rank)
         flat = buf.view(-1)
         len_hint = flen
+        if strong:
+            # the file's last frame carries the 800-B remainder: descriptor
+            # mode with the uniform geometry hint; only the rank holding it differs
+            last_pay = CFG4_FILE - (n_total - 1) * payload
+            d_off = torch.arange(n, device=dev, dtype=torch.int64) * stride
+            d_len = torch.full((n,), flen, dtype=torch.int32, device=dev)
+            if n and first + n == n_total:
+                content = last_pay + (8 if explicit else 0)
+                buf[n - 1, 2], buf[n - 1, 3] = content & 0xFF, content >> 8
+                d_len[n - 1] = 8 + content
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
     pay = torch.empty(n, dtype=torch.int32, device=dev) if args.pay else None
     nbad = torch.zeros(1, dtype=torch.int32, device=dev)
-    kw = dict(off=d_off, length=d_len, n=n, len_hint=len_hint) if ragged else dict(stride=stride, flen=flen, n=n)
+    desc = ragged or strong
+    kw = dict(off=d_off, length=d_len, n=n, len_hint=len_hint) if desc else dict(stride=stride, flen=flen, n=n)
     if args.verify:  # trailers must be valid first
         vc.frames(flat, out_crc=crc, **kw)
-        if ragged:
+        if desc:
             tidx = ((d_off + d_len.long())[:, None] + torch.arange(4, device=dev)[None, :]).reshape(-1)
             flat[tidx] = crc.view(torch.uint8)
         else:
@@ -279,7 +291,7 @@ def main():
     sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, 256, replace=False), [0, n - 1]]))
     from tests import _oracle
 
-    if ragged:
+    if desc:
         o = d_off.cpu().numpy()[sample_idx]
         l = d_len.cpu().numpy()[sample_idx].astype(np.int64)
         pieces = [flat[int(a):int(a) + int(b)].cpu().numpy() for a, b in zip(o, l)]
@@ -295,8 +307,9 @@ def main():
         parity = parity and int(nbad.item()) == 0
 
     # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
-    bytes_per_launch = int(d_len.long().sum().item()) if ragged else n * flen
-    total_bytes = (n_total * flen if strong else bytes_per_launch * world) * args.steps
+    bytes_per_launch = int(d_len.long().sum().item()) if desc else n * flen
+    file_crc_input = (n_total - 1) * flen + 8 + (CFG4_FILE - (n_total - 1) * payload) + (8 if explicit else 0)
+    total_bytes = (file_crc_input if strong else bytes_per_launch * world) * args.steps
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
@@ -380,7 +393,8 @@ def main():
             "config": {
                 "workload": (f"{args.config}: {n_total if strong else n} DATA frames x "
                              + (f"{CFG5_MIN}-{CFG5_MAX} B log-uniform payload (1 in 8 implied offset), packed unaligned"
-                                if ragged else f"{payload} B payload")
+                                if ragged else f"{payload} B payload"
+                                + (f" (last frame {CFG4_FILE - (n_total - 1) * payload} B: an 8 GiB file)" if strong else ""))
                              + (f" (one file, sharded over {world} GPU{'s' if world > 1 else ''}), " if strong else " per GPU, ")
                              + f"{'header_crc + ' if header else ''}trailer CRC-32"
                              f"{' (RX verify)' if args.verify else ''}"
