@@ -85,6 +85,19 @@ def test_region_dev(vc, dev, L):
         assert int(_u32(out)[0]) == _oracle.update_state(state_in, data)
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3, 5, 17])
+@pytest.mark.parametrize("L", [16385, 69633, 1_000_003, (16 << 20) + 9])
+def test_region_dev_misaligned(vc, dev, L, shift):
+    """k_region chunks are anchored at the window end; windows starting at any
+    byte (a resume window inside a file buffer) hash the same."""
+    data = _prng.prng_bytes(0xA11 + L + shift, L + shift)
+    d = torch.from_numpy(data).to(dev)
+    for state_in in (0xFFFFFFFF, 0x0BADCAFE):
+        out = vc.region(d[shift:], state_in)
+        torch.cuda.synchronize()
+        assert int(_u32(out)[0]) == _oracle.update_state(state_in, data[shift:])
+
+
 @pytest.mark.parametrize("piece", [65537, 1 << 20, 3 << 20])
 def test_region_chained_pieces(vc, dev, piece, monkeypatch):
     """Windows longer than one k_region launch covers (2^43 B) are chained

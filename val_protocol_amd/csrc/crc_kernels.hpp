@@ -409,7 +409,9 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
     group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
+#ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
+#endif
         if (PAY) lds_pow_write(cpim);
         __syncthreads();
         VCRC_STAMP(1);
