@@ -64,14 +64,17 @@ def workload(name, dev):
 
 
 def main():
+    """usage: ab_libs.py LIB_A LIB_B [LIB_C ...] [workload ...]: B, C, ... against A."""
     dev = torch.device("cuda:0")
-    libs = [load(sys.argv[1]), load(sys.argv[2])]
+    paths = [a for a in sys.argv[1:] if a.endswith(".so")]
+    names = [a for a in sys.argv[1:] if not a.endswith(".so")]
+    libs = [load(p) for p in paths]
     for l in libs:
         assert l.val_gpu_init(0) == 0
-    for name in sys.argv[3:] or ["cfg3", "cfg5"]:
+    for name in names or ["cfg3", "cfg5"]:
         w, nbytes = workload(name, dev)
         outs = []
-        res = [[], []]
+        res = [[] for _ in libs]
         for rep in range(4):
             for i, l in enumerate(libs):
                 vc._lib = l
@@ -84,11 +87,12 @@ def main():
                 res[i].append(med)
                 if rep == 0:
                     outs.append(out.clone())
-        same = bool(torch.equal(outs[0], outs[1]))
-        a, b = np.median(res[0]), np.median(res[1])
-        print(f"{name}: A {a:.4f} ms ({nbytes / a / 1e6:.0f} GB/s)  B {b:.4f} ms ({nbytes / b / 1e6:.0f} GB/s)  "
-              f"B/A speed {a / b:.3f}  same={same}  A={['%.3f' % x for x in res[0]]} B={['%.3f' % x for x in res[1]]}",
-              flush=True)
+        a = np.median(res[0])
+        line = f"{name}: A {a:.4f} ms ({nbytes / a / 1e6:.0f} GB/s)"
+        for i in range(1, len(libs)):
+            b = np.median(res[i])
+            line += (f"  {chr(65 + i)} {b:.4f} ms speed {a / b:.3f} same={bool(torch.equal(outs[0], outs[i]))}")
+        print(line, " ", [["%.3f" % x for x in r] for r in res], flush=True)
 
 
 if __name__ == "__main__":

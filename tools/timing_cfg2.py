@@ -46,6 +46,9 @@ print("  prologue dur", pct(us[:, 1] - us[:, 0]), " hash dur", pct(us[:, 2] - us
 blk = np.nonzero(used)[0] // 16
 end = us[:, 2]
 print("  end by blockIdx%8 (median us):", " ".join(f"{np.median(end[blk % 8 == x]):7.1f}" for x in range(8)))
+print("  start by blockIdx%8 (median us):", " ".join(f"{np.median(us[blk % 8 == x, 0]):7.2f}" for x in range(8)))
+print("  prologue end by blockIdx%8 (median us):", " ".join(f"{np.median(us[blk % 8 == x, 1]):7.2f}" for x in range(8)))
+print("  start by block (first 16 blocks, us):", " ".join(f"{us[blk == b, 0].min():5.2f}" for b in range(16)))
 slot = np.nonzero(used)[0] % 16
 print("  end by wave slot (median us):  ", " ".join(f"{np.median(end[slot == k]):6.0f}" for k in range(16)))
 per_block = np.array([end[blk == b].max() for b in np.unique(blk)])

@@ -29,7 +29,11 @@ namespace vcrc {
 // MI355X with uniform 3 GB batches (tools/sweep_lengths.py,
 // profiles/r01_length_sweep.log).
 constexpr int kClasses = 4;
-__host__ __device__ constexpr int class_lanes(int c) { return c == 0 ? 2 : c == 1 ? 4 : c == 2 ? 8 : 16; }
+#ifndef VCRC_CLASS_LANES  // A/B builds may override, e.g. -DVCRC_CLASS_LANES=4,8,16,16 (each >= the default: a
+#define VCRC_CLASS_LANES 2, 4, 8, 16  // bucket must stay inside one round of its class)
+#endif
+constexpr int kClassLanes[kClasses] = {VCRC_CLASS_LANES};
+__host__ __device__ constexpr int class_lanes(int c) { return c == 0 ? kClassLanes[0] : c == 1 ? kClassLanes[1] : c == 2 ? kClassLanes[2] : kClassLanes[3]; }
 __host__ __device__ inline int length_class(uint32_t L)
 {
     return L < 1024u ? 0 : L < 8192u ? 1 : L < 49152u ? 2 : 3;
