@@ -1,6 +1,7 @@
 """Randomised parity across every batch entry point (device and host memory,
 strided / descriptor-uniform / binned ragged / zero-copy / chunked, TX and
-verify, regions), each call checked bit-exact against the oracle. Seeded, so a
+verify, payload states, several logical GPUs, regions with random seeds),
+each call checked bit-exact against the oracle. Seeded, so a
 failure names a reproducible case; FUZZ_ROUNDS scales it."""
 import os
 
@@ -95,10 +96,29 @@ def test_fuzz_batches(vc, monkeypatch):
         ok_d, nbad_d = vc.verify_frames(torch.from_numpy(tr).to(dev), off=do, length=dl, len_hint=hint)
         torch.cuda.synchronize()
         assert int(nbad_d.item()) == want_bad and np.array_equal(ok_d.cpu().numpy(), want_ok), case + " verify dev"
-        # region over a random slice, device and host
+        # payload states (f4): raw zero-init register of each frame's payload
+        # (after the 8-B header and, when flags bit 0 is set, the 8-B offset)
+        ok_x, nbad_x, pay = vc.verify_frames_ex(torch.from_numpy(tr).to(dev), off=do, length=dl, len_hint=hint)
+        st_h, ok_h, nbad_h, pay_h = vc.verify_frames_ex_host(tr, offs, lens)
+        torch.cuda.synchronize()
+        want_pay = np.zeros(n, np.uint32)
+        for i, (o, L) in enumerate(zip(offs, lens)):
+            o, L = int(o), int(L)
+            pre = 16 if (L >= 8 and tr[o + 1] & 1) else 8
+            want_pay[i] = _oracle.update_state(0, tr[o + pre:o + L]) if L >= pre else 0
+        assert np.array_equal(pay.cpu().numpy().view(np.uint32), want_pay), case + " pay dev"
+        assert np.array_equal(pay_h, want_pay) and nbad_h == want_bad, case + " pay host"
+        assert int(nbad_x.item()) == want_bad and np.array_equal(ok_x.cpu().numpy(), want_ok), case + " verify ex"
+        # several logical GPUs from one process
+        ndev = int(rng.integers(2, 5))
+        assert np.array_equal(vc.frames_host_multi(base, offs, lens, ndev=ndev), want), case + f" multi {ndev}"
+        # region over a random slice, device and host, random seed
         a = int(rng.integers(0, base.size))
         b = int(rng.integers(a, base.size + 1))
         seg = base[a:b]
         want_r = _oracle.crc32(seg)
         assert (int(vc.region(d[a:b]).item()) & 0xFFFFFFFF) ^ 0xFFFFFFFF == want_r, case + f" region {a}:{b}"
         assert vc.val_crc32(seg) == want_r, case + f" host region {a}:{b}"
+        s0 = int(rng.integers(0, 1 << 32))
+        assert (int(vc.region(d[a:b], s0).item()) & 0xFFFFFFFF) == _oracle.update_state(s0, seg), case + " region seed"
+        assert vc.region_host_multi(seg, s0, ndev=ndev) == _oracle.update_state(s0, seg), case + " region multi"
