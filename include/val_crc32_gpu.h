@@ -64,7 +64,8 @@ int val_gpu_init_devices(int n);
 val_status_t val_gpu_set_device(int device);
 /* Device the calling thread's calls run on (-1: none initialised yet). */
 int val_gpu_current_device(void);
-/* Release every device context of the process. */
+/* Release every device context of the process (not concurrently with other
+ * calls of this library; contexts are re-created on the next call). */
 void val_gpu_shutdown(void);
 int val_gpu_device_count(void);
 uint32_t val_gpu_abi_version(void);

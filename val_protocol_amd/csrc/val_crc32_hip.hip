@@ -887,31 +887,34 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
 // (range % device count) and runs the single-device host path on it, writing
 // a disjoint range of the outputs. No collective, no peer traffic. Ranges
 // that share a device serialise on its context.
-void shard_frames(uint32_t n, const uint32_t *len, uint32_t flen, uint32_t world, uint32_t rank, uint32_t *start,
-                  uint32_t *count)
+// All world + 1 cuts in one pass: cut r = the first frame whose byte prefix
+// sum reaches total * r / world (count-balanced when len is NULL).
+std::vector<uint32_t> shard_cuts(uint32_t n, const uint32_t *len, uint32_t world)
 {
+    std::vector<uint32_t> cut(world + 1, n);
+    cut[0] = 0;
     if (!len) {
         const uint32_t base = n / world, extra = n % world;
-        *start = rank * base + std::min(rank, extra);
-        *count = base + (rank < extra ? 1u : 0u);
-        return;
+        for (uint32_t r = 1; r < world; r++) cut[r] = r * base + std::min(r, extra);
+        return cut;
     }
-    (void)flen;
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) total += len[i];
-    // cut r = first frame whose prefix sum reaches total * r / world
-    auto cut = [&](uint32_t r) -> uint32_t {
-        if (r == 0) return 0;
-        if (r >= world) return n;
+    uint64_t acc = 0;
+    uint32_t i = 0;
+    for (uint32_t r = 1; r < world; r++) {
         const uint64_t target = (uint64_t)((__uint128_t)total * r / world);
-        uint64_t acc = 0;
-        uint32_t i = 0;
         while (i < n && acc < target) acc += len[i++];
-        return i;
-    };
-    const uint32_t a = cut(rank), b = std::max(a, cut(rank + 1));
-    *start = a;
-    *count = b - a;
+        cut[r] = i;
+    }
+    return cut;
+}
+
+void shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t rank, uint32_t *start, uint32_t *count)
+{
+    const std::vector<uint32_t> cut = shard_cuts(n, len, world);
+    *start = cut[rank];
+    *count = cut[rank + 1] - cut[rank];
 }
 
 val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
@@ -926,10 +929,10 @@ val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uin
     std::vector<val_status_t> st(ndev, VAL_OK);
     std::vector<uint32_t> bad(ndev, 0);
     std::vector<std::string> err(ndev);
+    const std::vector<uint32_t> cut = shard_cuts(n, len, (uint32_t)ndev);
     auto work = [&](int d) {
         t_dev = d % count;  // more shards than devices share them round-robin
-        uint32_t s0, cnt;
-        shard_frames(n, len, flen, (uint32_t)ndev, (uint32_t)d, &s0, &cnt);
+        const uint32_t s0 = cut[d], cnt = cut[d + 1] - cut[d];
         const bool strided = off == nullptr;
         const uint8_t *b = strided ? base + (uint64_t)s0 * stride : base;
         const uint64_t bl = strided ? base_len - std::min<uint64_t>(base_len, (uint64_t)s0 * stride) : base_len;
@@ -1208,7 +1211,7 @@ void val_shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t 
         *start = *count = 0;
         return;
     }
-    shard_frames(n, len, 0, world, rank, start, count);
+    shard_frames(n, len, world, rank, start, count);
 }
 
 uint32_t val_crc32_init_state(void) { return 0xFFFFFFFFu; }
