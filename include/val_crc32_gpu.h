@@ -122,7 +122,7 @@ val_status_t val_crc32_verify_frames_ex_dev(const uint8_t *d_base, const uint64_
 
 /* Region CRC of one long device buffer: *d_state_out = raw register after
  * feeding d_ptr[0, len) to `state_in` (val_crc32_update_state semantics;
- * finalize with ^0xFFFFFFFF). One launch at any length: windows up to 16
+ * finalize with ^0xFFFFFFFF). One launch at any length: windows up to 8
  * KiB are one 64-lane frame; longer ones are chunked over the whole machine
  * and folded inside the same launch through a 128-byte library-owned device
  * accumulator, which calls on different streams share in turn (each call's

@@ -73,7 +73,7 @@ def test_regions_host(vc, golden):
 
 
 # ---- region (device) ---------------------------------------------------------
-@pytest.mark.parametrize("L", [0, 1, 2, 3, 4, 5, 7, 8, 63, 64, 65, 127, 128, 4095, 4096, 4097, 16383, 16384, 16385, 32768, 65535, 65536,
+@pytest.mark.parametrize("L", [0, 1, 2, 3, 4, 5, 7, 8, 63, 64, 65, 127, 128, 4095, 4096, 4097, 8191, 8192, 8193, 16384, 16385, 32768, 65535, 65536,
                                65537, 69632, 69633, 1_000_003, (16 << 20) - 1, 16 << 20, (16 << 20) + 1,
                                (64 << 20) + 7, 16 * 4096 * 4096 + 4096 * 17 + 3])
 def test_region_dev(vc, dev, L):

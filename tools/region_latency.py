@@ -20,7 +20,7 @@ big = torch.randint(0, 256, (256 << 20,), dtype=torch.uint8, device=dev, generat
 stream = torch.cuda.current_stream()
 out = torch.empty(1, dtype=torch.int32, device=dev)
 rows = []
-for size in (1 << 10, 8 << 10, 16 << 10, 32 << 10, (32 << 10) + 1, 48 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20, 256 << 20):
+for size in (1 << 10, 4 << 10, 8 << 10, (8 << 10) + 1, 16 << 10, (16 << 10) + 1, 32 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20, 256 << 20):
     win = big[:size]
     vc.region(win, out=out)
     torch.cuda.synchronize()

@@ -405,7 +405,7 @@ hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 // fold); longer windows go to k_region with chunks of W = 2^k0 >= 4 KiB,
 // doubling until there are at most 4,096 chunks (one per wave of the
 // machine; 256 MiB = 4,096 chunks of 64 KiB = 16 rounds per lane).
-constexpr uint64_t kRegionOneFrame = 16u << 10;  // one 64-lane frame of <= 4 rounds; k_region is faster above (tools/region_latency.py: 32 KiB 12.1 us as one frame, 10.1 us in k_region)
+constexpr uint64_t kRegionOneFrame = 8u << 10;  // one 64-lane frame of <= 2 rounds; k_region is faster above (profiles/r02_region_latency.log: 16 KiB 8.9 us as one frame, 8.2 us in k_region)
 constexpr uint64_t kRegionMaxPiece = (uint64_t)kRegionMaxChunks << 31;  // W <= 2^31: longer windows chain pieces
 void region_geometry(uint64_t len, uint64_t *W, uint32_t *k0, uint32_t *C)
 {
