@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling target for small batches (run under rocprofv3 --kernel-trace):
 for each workload x geometry, REPS launches with a sync after each.
-usage: prof_small.py REPS name:G:PF ...   (G 0 / PF -1 = automatic). Tooling only."""
+usage: [VCRC_LIB=lib.so] prof_small.py REPS name:G:PF ...   (G 0 / PF -1 = automatic). Tooling only."""
 import os
 import sys
 
@@ -9,7 +9,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import val_protocol_amd.crc as vc  # noqa: E402
-from tools.ab_libs import workload  # noqa: E402
+from tools.ab_libs import load, workload  # noqa: E402
+
+if os.environ.get("VCRC_LIB"):  # another build of the library (A/B)
+    vc._lib = load(os.environ["VCRC_LIB"])
 
 reps = int(sys.argv[1])
 dev = torch.device("cuda:0")
