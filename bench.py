@@ -182,6 +182,33 @@ def read_pmc_traffic(config: str):
         return None
 
 
+def read_roof(torch, flat, stream):
+    """Same-box achievable read rate (GB/s): a plain read-only stream over this
+    run's frame buffer (bench/roof.hip, built by __graft_entry__.build()), timed
+    with events on the stream it runs on. None if the helper is not built."""
+    so = os.path.join(ROOT, "bench", "libval_roof.so")
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    lib.val_bench_read_roof.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    lib.val_bench_read_roof.restype = ctypes.c_int
+    sink = torch.zeros(1, dtype=torch.int32, device=flat.device)
+    nbytes = (flat.numel() // 128) * 128
+    go = lambda: lib.val_bench_read_roof(flat.data_ptr(), nbytes, sink.data_ptr(), stream.cuda_stream)  # noqa: E731
+    if go() != 0:
+        return None
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        go()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    return nbytes / (float(np.median(ms)) * 1e-3) / 1e9
+
+
 def main():
     args = parse()
     import torch
@@ -313,6 +340,7 @@ def main():
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
+    roof = read_roof(torch, flat, stream) if rank == 0 else None
 
     if args.host_inclusive and rank == 0 and not ragged:
         host = buf.cpu().numpy().reshape(-1)
@@ -418,6 +446,9 @@ def main():
                 "traffic": traffic,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": bytes_per_launch,
+                # same box, same buffer: plain read-only stream (bench/roof.hip); SURVEY 8(d)
+                "read_roof": round(roof, 1) if roof else None,
+                "frac_of_read_roof": round(achieved_gbs / roof, 4) if roof else None,
             },
             "cpu_baseline": cpu,
         }
