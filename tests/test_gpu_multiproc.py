@@ -1,0 +1,103 @@
+"""World-size-2 runs of the N > 1 paths on one GPU (both ranks on cuda:0,
+gloo for the host-side collectives), with every CRC computed by the product:
+  * bench.py under torch.distributed.run, as the driver launches it for
+    --gpus N: weak scaling (cfg2, each rank its own batch) and strong scaling
+    (cfg4, one 8 GiB file sharded by contiguous frame ranges, the last frame
+    800 B on the last rank);
+  * a window split into per-rank byte ranges (val_protocol_amd.shard, the
+    product's val_shard_region rule), each rank's partial register computed by
+    val_crc32_region_dev on the GPU, gathered over gloo and folded with the
+    product's val_crc32_fold_partials, against the oracle.
+SURVEY 8(e); reference window fill src/val_sender.c:822-841."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench_two_ranks(config: str) -> dict:
+    env = dict(os.environ, VAL_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_weak_cfg2():
+    line = _bench_two_ranks("cfg2")
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["parity_sample_ok"] is True
+    assert line["config"]["frames_per_gpu"] == 65536
+    assert line["value"] > 0 and line["cpu_baseline"] is None
+
+
+def test_bench_two_ranks_strong_cfg4():
+    line = _bench_two_ranks("cfg4")
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["parity_sample_ok"] is True
+    assert line["config"]["frames_total"] == 131113
+    assert line["config"]["frames_per_gpu"] in (65556, 65557)  # rank 0's byte-balanced share
+
+
+def _region_worker(rank, world, port, data, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import val_protocol_amd.crc as vc
+    from val_protocol_amd.shard import fold_partials, shard_region
+
+    vc.init(0)
+    dev = torch.device("cuda:0")
+    start, cnt = shard_region(data.size, world, rank, align=64)
+    d = torch.from_numpy(np.ascontiguousarray(data[start:start + cnt])).to(dev)
+    st = int(vc.region(d, state_in=0xFFFFFFFF if rank == 0 else 0).item()) & 0xFFFFFFFF
+    torch.cuda.synchronize()
+    t = torch.tensor([st, cnt], dtype=torch.int64)
+    out = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(out, t)
+    if rank == 0:
+        q.put((fold_partials([(int(o[0]), int(o[1])) for o in out]) ^ 0xFFFFFFFF, vc.cpu_fallback_count()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nbytes", [1_000_003, 9 << 20])
+def test_region_split_fold_gpu_ranks(nbytes):
+    import torch.multiprocessing as mp
+
+    from tests import _oracle, _prng
+
+    data = _prng.prng_bytes(0xD16 + nbytes, nbytes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_region_worker, args=(r, 2, port, data, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    got, fallbacks = q.get(timeout=10)
+    assert fallbacks == 0
+    assert got == _oracle.crc32(data)
