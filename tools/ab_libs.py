@@ -31,6 +31,10 @@ def workload(name, dev):
         n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    if name.startswith("w") and "x" in name:  # wNNNxLLLLL: a window of NNN strided frames of LLLLL CRC bytes
+        n, L = (int(v) for v in name[1:].split("x"))
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
     if name.startswith("s") and name[1:].isdigit():  # sNNNNN: 1 M strided frames of NNNNN CRC bytes, stride +4
         n, L = 1 << 20, int(name[1:])
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

@@ -697,6 +697,94 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     }
 }
 
+// ---- K1/K2 for small batches of long frames: one workgroup per frame --------
+// A batch of a few long frames leaves most of the machine idle even at one
+// wave per frame, and each wave walks its frame one 4 KiB round after
+// another (256 x 64 KiB: 16 rounds, ~40 us). Here a workgroup takes a whole
+// frame: the frame is cut into chunks of W = 2^k0 bytes anchored at its end
+// (only chunk 0 can be short; it carries the seed), the 16 waves hash 16
+// chunks at a time as k_region's waves do (hash_frame at 64 lanes), wave 0
+// folds their registers (4-level shuffle tree, LDS maps "advance W * 2^j"),
+// and a frame longer than 16 W folds its 16-chunk groups front to back
+// ("advance 16 W"). A padded chunk holds zeros, which are inert. Lane 15 of
+// wave 0 writes the trailer CRC and, on verify, compares the stored LE32; it
+// also hashes the frame's first 8 bytes for header_crc (chunk 0 can be
+// shorter than the header). Uniform and descriptor batches alike (any length
+// per frame).
+__global__ __launch_bounds__(kBlock) void k_frames_split(const FrameParams p, const uint32_t k0)
+{
+    __shared__ uint32_t s_fold[kWavesPerBlock];
+    LdsImage im;
+    lds_tables_issue(p.consts, im);
+    PowImage pim;
+    lds_pow_issue(p.consts, k0, pim);
+    lds_tables_write(im);
+    lds_pow_write(pim);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wi = threadIdx.x >> 6;
+    const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
+    const uint64_t W = (uint64_t)1 << k0;
+    for (uint64_t f = blockIdx.x; f < p.n; f += gridDim.x) {
+        uint64_t off = 0;
+        uint32_t L = 0;
+        frame_desc(p, f, off, L);
+        const uint64_t C = L ? ((uint64_t)L + W - 1) >> k0 : 1u;  // chunks
+        const uint64_t groups = (C + kWavesPerBlock - 1) / kWavesPerBlock;
+        FrameParams q{};
+        q.base = p.base;
+        q.n = (uint32_t)C;
+        q.seed0 = f == 0 ? p.seed0 : p.seed_rest;
+        q.seed_rest = 0;
+        q.xorout = p.xorout;  // finishes header_crc; the chunk registers come back raw (no out_crc)
+        q.consts = p.consts;
+        uint32_t facc = 0;  // wave 0, lane 15: the frame's register over the groups so far
+        for (uint64_t g = 0; g < groups; g++) {
+            // group g: chunks C - (groups - g) * 16 + wi, the first group padded at the front
+            const int64_t cp = (int64_t)C - (int64_t)(groups - g) * kWavesPerBlock + wi;
+            const bool real = cp >= 0;
+            const uint64_t c = real ? (uint64_t)cp : 0u;
+            const uint64_t hi = (uint64_t)L - (C - 1u - c) * W;
+            const uint64_t lo = hi > W ? hi - W : 0u;
+            const uint32_t st = hash_frame<64, 1, false, true>(q, c, real, off + lo, real ? (uint32_t)(hi - lo) : 0u,
+                                                             lane, sb, 64, [] {});
+            if (lane == 63) s_fold[wi] = real ? st : 0u;
+            __syncthreads();
+            if (wi == 0) {
+                uint32_t v = lane < kWavesPerBlock ? s_fold[lane] : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t other = __shfl_xor(v, 1 << j);
+                    const bool right = (lane >> j) & 1;
+                    const uint32_t left = right ? other : v;
+                    v = map_apply(left, pow_map(j)) ^ (right ? v : other);
+                }
+                facc = g ? map_apply(facc, pow_map(4)) ^ v : v;  // a later group is 16 W bytes long
+            }
+            __syncthreads();  // s_fold is reused by the next group
+        }
+        if (wi == 0 && lane == kWavesPerBlock - 1) {
+            const uint32_t crc = facc ^ p.xorout;
+            if (p.out_crc) p.out_crc[f] = crc;
+            if (p.out_hdr) {
+                gu8 *fp = gptr(p.base) + off;
+                uint32_t h = q.seed0;
+                if (L >= 8) {
+                    h = s4_step(h, ld32(fp), sb);
+                    h = s4_step(h, ld32(fp + 4), sb);
+                } else {
+                    for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
+                }
+                p.out_hdr[f] = h ^ p.xorout;
+            }
+            if (p.verify) {
+                const bool good = crc == ld32(gptr(p.base) + off + L);
+                if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
+                if (!good && p.nbad) atomicAdd(p.nbad, 1u);
+            }
+        }
+    }
+}
+
 // ---- K4: region CRC, one launch --------------------------------------------
 // A long window of len bytes is cut into C chunks of W = 2^k0 bytes (k0 >= 12)
 // anchored at the window END: chunk c covers [len - (C-c) W, len - (C-c-1) W),

@@ -195,15 +195,18 @@ uint32_t lanes_per_frame(uint32_t len)
 // G for a uniform batch of n frames of len bytes: the class's G, doubled while
 // the batch would leave more than half of the machine's waves idle (a small
 // window spreads each frame over more lanes, so its serial chain is shorter),
-// up to 16 lanes (64 for a batch of at most 16 frames) and at most one 64-B
-// unit per lane per round.
+// up to one wave per frame and at most one 64-B unit per lane per round. The
+// doubling only acts on batches of fewer groups than half the machine's waves
+// (one pass of the grid); large batches keep the class's measured G. Capping
+// it at 16 cost small windows of long frames 1.5-2.5x (256 x 64 KiB: 103 ->
+// 41 us per call; 256 x 16 KiB: 34 -> 20 us; profiles/r02_ab_lanes_cap.log).
 uint32_t lanes_for_batch(const Ctx &c, uint32_t len, uint64_t n)
 {
     uint32_t G = lanes_per_frame(len);
     if (forced_lanes()) return G;
     const uint64_t waves = (uint64_t)c.cus * kWavesPerBlock;
     const uint64_t units = len ? (len + kUnit - 1) / kUnit : 1u;
-    const uint32_t cap = n <= 16 ? 64u : 16u;  // a lone frame (scalar hooks, small regions) takes a whole wave
+    const uint32_t cap = 64u;
     while (G < cap && 2u * G <= units && (n + 64 / G - 1) / (64 / G) * 2u <= waves) G *= 2;
     return G;
 }
@@ -242,6 +245,46 @@ void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
     case 4: hipLaunchKernelGGL((k_frames<G, 4, false>), grid, dim3(kBlock), 0, s, p); break;
     default: hipLaunchKernelGGL((k_frames<G, 1, false>), grid, dim3(kBlock), 0, s, p); break;
     }
+}
+
+// Small batches of long frames go to k_frames_split (one workgroup per frame,
+// its chunks hashed by 16 waves at once) when that takes fewer memory rounds
+// per wave than one wave per frame: ceil(n / CUs) passes of about three
+// round-times each (a chunk round, the fold, the next frame's start) against
+// ceil(units / 64) rounds. Measured (profiles/r02_ab_split.log): 256 x 64 KiB
+// 41 -> 18 us per call, 256 x 8 KiB 21.5 -> 16 us, equal at 1024 x 64 KiB,
+// slower at 2048 x 64 KiB and 512 x 16 KiB (the rule keeps those off it).
+// Payload states and forced geometries keep the frames kernels.
+// VAL_GPU_SPLIT=0 disables it.
+bool split_enabled()
+{
+#ifdef VCRC_NO_SPLIT  // A/B builds only
+    return false;
+#endif
+    static const bool on = !(getenv("VAL_GPU_SPLIT") && atoi(getenv("VAL_GPU_SPLIT")) == 0);
+    return on;
+}
+
+bool use_split(const Ctx &c, const FrameParams &p, uint32_t len)
+{
+    if (!split_enabled() || p.out_pay || forced_lanes() || forced_prefetch() >= 0 || len < 8192u) return false;
+    const uint64_t waves = (uint64_t)c.cus * kWavesPerBlock;
+    if ((uint64_t)p.n * 2u > waves) return false;
+    const uint64_t rounds = ((uint64_t)len / kUnit + 1u + 63u) / 64u;  // at one wave per frame
+    const uint64_t passes = ((uint64_t)p.n + c.cus - 1u) / (uint64_t)c.cus;
+    return passes * 3u <= rounds;
+}
+
+val_status_t launch_split(const Ctx &c, FrameParams &p, uint32_t len, hipStream_t s)
+{
+    p.consts = c.d_consts;
+    // W = 2^k0 >= 1 KiB with a typical frame in at most 16 chunks (one group)
+    uint32_t k0 = 10;
+    while (((uint64_t)kWavesPerBlock << k0) < (uint64_t)len && k0 < 31) k0++;
+    const dim3 grid((unsigned)std::min<uint64_t>(p.n, (uint64_t)c.cus));
+    hipLaunchKernelGGL(k_frames_split, grid, dim3(kBlock), 0, s, p, k0);
+    VCRC_HIP(hipGetLastError(), "k_frames_split launch");
+    return VAL_OK;
 }
 
 val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, hipStream_t s)
@@ -395,7 +438,10 @@ val_status_t launch_frames(Ctx &c, FrameParams &p, uint32_t typical_len, hipStre
 {
     if (p.n == 0) return VAL_OK;
     if (p.off && typical_len == 0 && !forced_lanes() && p.n >= ragged_min_frames()) return launch_ragged(c, p, s);
-    return launch_uniform(c, p, lanes_for_batch(c, typical_len ? typical_len : 16384u, p.n), s);
+    const uint32_t len = typical_len ? typical_len : 16384u;
+    const uint32_t longest = !p.off ? std::max(p.flen, p.last_len) : len;
+    if (use_split(c, p, longest)) return launch_split(c, p, longest, s);
+    return launch_uniform(c, p, lanes_for_batch(c, len, p.n), s);
 }
 
 // NULL selects the HIP default (null) stream, as in every HIP API.
