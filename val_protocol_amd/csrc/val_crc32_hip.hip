@@ -314,7 +314,7 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, hipStr
 // 8.002 wave-rounds, the last one 99.8% idle. The frames of a partial last
 // round are re-cut with more lanes per frame (up to 64) into a second launch
 // on the same stream, so the tail costs about G / G_tail of a group-time.
-val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, hipStream_t s)
+val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t len, hipStream_t s)
 {
     const uint64_t per = 64 / G, groups = (p.n + per - 1) / per;
     const uint64_t waves = (uint64_t)c.cus * kWavesPerBlock;
@@ -340,7 +340,12 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, hipStream_
     if (p.out_ok) t.out_ok = p.out_ok + n_main;
     if (p.out_pay) t.out_pay = p.out_pay + n_main;
     val_status_t st = launch_uniform_one(c, m, G, s);
-    return st == VAL_OK ? launch_uniform_one(c, t, Gt, s) : st;
+    if (st != VAL_OK) return st;
+    // a tail of a few long frames (cfg4: 41 x 64 KiB after 8 full rounds) is a
+    // small batch of its own: one workgroup per frame when that is faster
+    const uint32_t tl = t.off ? len : std::max(t.flen, t.last_len);
+    if (use_split(c, t, tl)) return launch_split(c, t, tl, s);
+    return launch_uniform_one(c, t, Gt, s);
 }
 
 // Ragged descriptor batch: counting-sort by length on the device, then one
@@ -441,7 +446,7 @@ val_status_t launch_frames(Ctx &c, FrameParams &p, uint32_t typical_len, hipStre
     const uint32_t len = typical_len ? typical_len : 16384u;
     const uint32_t longest = !p.off ? std::max(p.flen, p.last_len) : len;
     if (use_split(c, p, longest)) return launch_split(c, p, longest, s);
-    return launch_uniform(c, p, lanes_for_batch(c, len, p.n), s);
+    return launch_uniform(c, p, lanes_for_batch(c, len, p.n), len, s);
 }
 
 // NULL selects the HIP default (null) stream, as in every HIP API.
