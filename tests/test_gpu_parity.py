@@ -538,3 +538,30 @@ def test_wave_round_tail(vc, dev, L, extra):
     torch.cuda.synchronize()
     okh = ok.cpu().numpy()
     assert int(nbad.item()) == 1 and int(okh.argmin()) == bad and int(okh.sum()) == n - 1
+
+
+@pytest.mark.parametrize("strided", [True, False])
+def test_dynamic_tail_every_frame(vc, dev, strided):
+    """Launches long enough for the dynamic tail (k_frames: the last half of
+    the group rounds come from a queue): 4 full rounds of the machine plus a
+    partial one, every frame checked against the oracle, then the same batch
+    again (the queue must have been re-zeroed by the previous launch)."""
+    vc.set_geometry()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    payload = 65516 if not strided else 16384           # descriptor groups of 4 x 64 KiB, strided 8 x 16 KiB
+    per = 4 if not strided else 8
+    n = cus * 16 * per * 4 + 777
+    flen = 8 + 8 + payload
+    stride = flen + 4
+    g = torch.Generator(device=dev).manual_seed(11)
+    buf = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
+    kw = dict(stride=stride, flen=flen, n=n) if strided else dict(
+        off=torch.arange(n, device=dev, dtype=torch.int64) * stride,
+        length=torch.full((n,), flen, dtype=torch.int32, device=dev), len_hint=flen)
+    host = buf.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    want = _oracle.frames(host, offs, np.full(n, flen, np.uint32), nthreads=16)
+    for _ in range(2):
+        crc = vc.frames(buf, **kw)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u32(crc), want)

@@ -27,6 +27,11 @@ def workload(name, dev):
         n, L = {"cfg2": (1 << 16, 1040), "cfg4": (131113, 65532), "w256": (256, 1040)}[name]
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    if name == "cfg4d":  # cfg4 as bench.py launches it: descriptors with the uniform length hint
+        n, L = 131113, 65532
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        off = torch.arange(n, device=dev, dtype=torch.int64) * (L + 4)
+        return dict(buf=buf, off=off, length=torch.full((n,), L, dtype=torch.int32, device=dev), len_hint=L), n * L
     if name in ("cfg3", "cfg3b"):  # cfg3b: the bench layout (flen 16400, stride 16404)
         n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

@@ -61,6 +61,8 @@ struct FrameParams {
     uint32_t *bin_counts;    // ragged mode: k_bin_count's bucket totals, re-zeroed here for the next batch
     const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
     uint32_t *out_pay;       // RX by-product: raw zero-init register of each frame's payload (nullable)
+    uint32_t *qhead;         // uniform mode: dynamic-tail queue {head, exits} (zero on entry, re-zeroed), nullable
+    uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -443,8 +445,37 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         __syncthreads();
         VCRC_STAMP(1);
     });
-    while (fb < p.n) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    if (!p.qhead) {
+        while (fb < p.n) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+        VCRC_STAMP(2);
+        return;
+    }
+    // Dynamic tail: the first static_rounds group rounds are dealt as above,
+    // the rest are pulled one group at a time from a queue, so waves that run
+    // ahead (the oldest of a SIMD issue first) take more of the end. The last
+    // wave out re-zeroes the queue for the next launch on this stream.
+    const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
+    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&p.qhead[0], 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        const uint64_t gb = dyn + (uint64_t)k * kGroups;
+        if (gb >= p.n) break;
+        const uint64_t fd = gb + (uint64_t)(lane / G);
+        uint64_t od = 0;
+        uint32_t Ld = 0;
+        if (fd < p.n) frame_desc(p, fd, od, Ld);
+        hash_frame<G, PF, PAY, false>(p, fd, fd < p.n, od, Ld, lane % G, sb, G, [] {});
+    }
     VCRC_STAMP(2);
+    if (lane == 0) {
+        const uint32_t out = atomicAdd(&p.qhead[16], 1u);
+        if (out == (uint32_t)nwaves - 1u) {  // every wave is past its last dequeue
+            atomicExch(&p.qhead[0], 0u);
+            atomicExch(&p.qhead[16], 0u);
+        }
+    }
 }
 
 // ---- ragged path ------------------------------------------------------------

@@ -41,6 +41,7 @@ struct StreamScratch {
     hipStream_t stream;
     Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin;     // ragged binning: counts, plan, sorted order
+    Arena queue;   // k_frames dynamic tail {head, exits} (zero between calls)
 };
 
 // One context per HIP device: streams, constant blob, staging and scratch.
@@ -247,6 +248,23 @@ void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
     }
 }
 
+StreamScratch &scratch_for(Ctx &c, hipStream_t s);
+val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out);
+
+// Dynamic tail of long uniform launches (k_frames): VAL_GPU_DYNAMIC_TAIL=0/1.
+#ifndef VCRC_DYN_MIN_ROUNDS
+#define VCRC_DYN_MIN_ROUNDS 4
+#endif
+#ifndef VCRC_DYN_TAIL_DEFAULT
+#define VCRC_DYN_TAIL_DEFAULT 1
+#endif
+bool dyn_tail_enabled()
+{
+    static const bool on = getenv("VAL_GPU_DYNAMIC_TAIL") ? atoi(getenv("VAL_GPU_DYNAMIC_TAIL")) != 0
+                                                         : VCRC_DYN_TAIL_DEFAULT != 0;
+    return on;
+}
+
 // Small batches of long frames go to k_frames_split (one workgroup per frame,
 // its chunks hashed by 16 waves at once) when that takes fewer memory rounds
 // per wave than one wave per frame: ceil(n / CUs) passes of about three
@@ -287,7 +305,7 @@ val_status_t launch_split(const Ctx &c, FrameParams &p, uint32_t len, hipStream_
     return VAL_OK;
 }
 
-val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, hipStream_t s)
+val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32_t len, hipStream_t s)
 {
     p.consts = c.d_consts;
     const uint64_t groups_per_block = (uint64_t)kWavesPerBlock * (64 / G);
@@ -295,6 +313,31 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, hipStr
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
     const int pf = prefetch_depth();
+    // dynamic tail for long launches: the last 1/8 of the group rounds (at
+    // least one) come from a queue (k_frames)
+    const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * kWavesPerBlock);
+    p.qhead = nullptr;
+    // a group must be long enough that the one queue word is not the limit
+    // (it serves ~88 dequeues/us): 4,096 waves over >= 128 KiB groups is
+    // about 48/us at 6 TB/s; descriptor batches, whose queued groups load
+    // their descriptors behind the dequeue, need more (u16400d: -4% at
+    // 131 KB groups; cfg4's 4 x 64 KiB groups gain)
+    const uint64_t group_bytes = (uint64_t)(64 / G) * len;
+    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && group_bytes >= (p.off ? 192u << 10 : 128u << 10)) {
+        Ctx &cm = const_cast<Ctx &>(c);
+        std::lock_guard<std::recursive_mutex> lk(cm.mu);
+        Arena &a = scratch_for(cm, s).queue;
+        uint8_t *q = nullptr;
+        val_status_t st = arena_acquire(a, 128, s, &q);
+        if (st != VAL_OK) return st;
+        if (!a.counts_zero) VCRC_HIP(hipMemsetAsync(q, 0, 128, s), "hipMemsetAsync(queue)");
+        a.counts_zero = true;  // the last wave out re-zeroes it
+        p.qhead = reinterpret_cast<uint32_t *>(q);
+#ifndef VCRC_DYN_DIV
+#define VCRC_DYN_DIV 2
+#endif
+        p.static_rounds = (uint32_t)(VCRC_DYN_DIV == 1 ? 1u : rounds - std::max<uint64_t>(1, rounds / VCRC_DYN_DIV));
+    }
     switch (G) {
     case 1: launch_uniform_g<1>(pf, grid, s, p); break;
     case 2: launch_uniform_g<2>(pf, grid, s, p); break;
@@ -323,7 +366,7 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t l
     const uint64_t n_main = full * waves * per, n_tail = p.n - std::min<uint64_t>(p.n, n_main);
     if (full > 0 && n_tail > 0)
         while (Gt < 64 && (n_tail + 64 / (2 * Gt) - 1) / (64 / (2 * Gt)) <= waves) Gt *= 2;
-    if (Gt == G) return launch_uniform_one(c, p, G, s);
+    if (Gt == G) return launch_uniform_one(c, p, G, len, s);
     FrameParams m = p, t = p;
     m.n = (uint32_t)n_main;
     t.n = (uint32_t)n_tail;
@@ -339,13 +382,13 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t l
     if (p.out_hdr) t.out_hdr = p.out_hdr + n_main;
     if (p.out_ok) t.out_ok = p.out_ok + n_main;
     if (p.out_pay) t.out_pay = p.out_pay + n_main;
-    val_status_t st = launch_uniform_one(c, m, G, s);
+    val_status_t st = launch_uniform_one(c, m, G, len, s);
     if (st != VAL_OK) return st;
     // a tail of a few long frames (cfg4: 41 x 64 KiB after 8 full rounds) is a
     // small batch of its own: one workgroup per frame when that is faster
     const uint32_t tl = t.off ? len : std::max(t.flen, t.last_len);
     if (use_split(c, t, tl)) return launch_split(c, t, tl, s);
-    return launch_uniform_one(c, t, Gt, s);
+    return launch_uniform_one(c, t, Gt, tl, s);
 }
 
 // Ragged descriptor batch: counting-sort by length on the device, then one
@@ -354,7 +397,7 @@ StreamScratch &scratch_for(Ctx &c, hipStream_t s)
 {
     for (StreamScratch *x : c.scratch)
         if (x->stream == s) return *x;
-    c.scratch.push_back(new StreamScratch{s, {}, {}});
+    c.scratch.push_back(new StreamScratch{s, {}, {}, {}});
     return *c.scratch.back();
 }
 
@@ -1102,6 +1145,7 @@ void ctx_free(Ctx &c)
     (void)hipDeviceSynchronize();  // the streams that used the scratch may be gone
     for (StreamScratch *x : c.scratch) {
         arena_free(x->region);
+        arena_free(x->queue);
         arena_free(x->bin);
         delete x;
     }
