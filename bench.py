@@ -42,7 +42,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=15)  # the first ~10 cfg3 launches run 1-4% slower (clocks settling)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--verify", action="store_true", help="time the RX verify kernel instead of TX")
     ap.add_argument("--pay", action="store_true", help="with --verify: also emit payload states (RX file-CRC by-product)")
@@ -308,7 +308,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    step_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_ms = float(np.mean(step_ms))
+    print("[bench] per-step ms: " + " ".join(f"{x:.4f}" for x in step_ms), file=sys.stderr)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
