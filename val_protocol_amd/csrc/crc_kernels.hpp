@@ -375,6 +375,17 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
 
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
 __device__ uint64_t g_vcrc_time[4096 * 4];
+__device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lane 0's frame in the wave's last item
+#define VCRC_LAST_ITEM(c_, L_)                                                                                  \
+    do {                                                                                                        \
+        const uint64_t w_ = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;                                 \
+        const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                                   \
+        const uint32_t l_ = __shfl((uint32_t)(L_), 0);                                                          \
+        if ((threadIdx.x & 63) == 0 && w_ < 4096) {                                                             \
+            g_vcrc_time[w_ * 4 + 3] = t_;                                                                       \
+            g_vcrc_info[w_] = ((uint32_t)(c_) << 16) | (l_ >> 6);                                               \
+        }                                                                                                       \
+    } while (0)
 #define VCRC_STAMP(k)                                                                                      \
     do {                                                                                                   \
         const uint64_t w_ = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;                            \
@@ -383,6 +394,9 @@ __device__ uint64_t g_vcrc_time[4096 * 4];
 #else
 #define VCRC_STAMP(k) \
     do {              \
+    } while (0)
+#define VCRC_LAST_ITEM(c_, L_) \
+    do {                       \
     } while (0)
 #endif
 
@@ -490,6 +504,13 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 //   class 2 (G=8,  512 B rounds): L in [8192, 49152)   buckets 37..117
 //   class 3 (G=16, 1 KiB rounds): L in [49152, 65536]  buckets 118..134, longer 135
 constexpr int kBuckets = 136;
+// Work-queue partitions of the ragged kernel (one head word each, 64 B apart;
+// the host sizes the heads scratch from this).
+#ifndef VCRC_RAGGED_PARTS  // A/B builds may override
+#define VCRC_RAGGED_PARTS 64  // 1, 2, 4 partitions: slower (u1100 up to 2.8x); 8 -> 64: +1.5-3% (r02_ab_ragged_parts.log)
+#endif
+constexpr uint32_t kQueueParts = VCRC_RAGGED_PARTS;
+static_assert(kQueueParts >= 1 && kQueueParts <= 64, "queue partitions");
 __host__ __device__ inline int length_bucket(uint32_t L)
 {
     if (L < 1024u) return L <= 128u ? 0 : (int)((L - 1u) / 128u);
@@ -601,7 +622,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_scatter(const uint32_t *len
     if (threadIdx.x < 64) bin_starts_wave(gcount, cur);
     __syncthreads();
     if (blockIdx.x == 0) {
-        if (threadIdx.x < 8u * 16u) heads[threadIdx.x] = 0u;
+        for (uint32_t i = threadIdx.x; i < kQueueParts * 16u; i += blockDim.x) heads[i] = 0u;
         if (threadIdx.x == 0) {
             // class cc = the sorted range from its longest bucket's start to the
             // next shorter class's (class 0 ends at n: every frame has a bucket);
@@ -662,10 +683,11 @@ __device__ __forceinline__ void item_frame(const FrameParams &p, const Item &t, 
 // Ragged batches: persistent grid; waves pull items (64/G frames of one
 // class, longest first) from a work queue, so the launch ends about one item
 // after the bytes run out (longest-processing-time-first: a static cyclic deal
-// gave wave 0 the longest item of every round). The queue is split into P <= 8
-// interleaved partitions (item = part + P * k), one head word each, keyed by
-// blockIdx % P -- on MI355X that is the workgroup's XCD, so a head is only
-// pulled by the 512 waves of one XCD (one word saturates near 88 dequeues/us).
+// gave wave 0 the longest item of every round). The queue is split into
+// P <= kQueueParts (64) interleaved partitions (item = part + P * k), one head
+// word each, keyed by blockIdx % P: a head is pulled by the 64 waves of four
+// workgroups on one XCD (one word saturates near 88 dequeues/us; 8 heads, one
+// per XCD, measured 1.5-3% slower on every mix and one head up to 2.8x).
 // Every partition has at least one workgroup (P <= gridDim.x), so every item
 // is hashed exactly once whatever the placement. A wave's first two items are
 // static; item i + 2 is dequeued while item i hashes and item i + 1's
@@ -687,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     const uint32_t items = ctab[12];
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
-    const uint32_t P = min(8u, gridDim.x);
+    const uint32_t P = min(kQueueParts, gridDim.x);
     const uint32_t part = blockIdx.x % P;
     const uint32_t nwp = ((gridDim.x - part + P - 1) / P) * kWavesPerBlock;  // waves of this partition
     uint32_t *head = p.heads + part * 16u;  // 64 B apart
@@ -713,6 +735,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
             item_frame(p, nxt, lane, f_n, active_n, off_n, L_n);
         }
         const int G = class_lanes(cur.c);
+        VCRC_LAST_ITEM(cur.c, L);
         hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
         if (it_n >= items) {
             VCRC_STAMP(2);

@@ -431,10 +431,10 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
     const uint32_t n = p.n;
     const uint32_t nbin = std::max(1u, std::min(1024u, (n + 2047u) / 2048u));
     const uint32_t chunk = (n + nbin - 1) / nbin;
-    // scratch: heads[8][16] u32 | gcount[kBuckets] u32 | ctab[16] u32 | blockoff[nbin][kBuckets] u32 |
+    // scratch: heads[kQueueParts][16] u32 | gcount[kBuckets] u32 | ctab[16] u32 | blockoff[nbin][kBuckets] u32 |
     //          order[n] u32. gcount is zero between batches (k_frames_ragged re-zeroes it once
     //          k_bin_scatter has read it); heads are zeroed by k_bin_scatter.
-    const size_t sz_heads = 8u * 64u, sz_gcount = (size_t)kBuckets * 4u;
+    const size_t sz_heads = (size_t)kQueueParts * 64u, sz_gcount = (size_t)kBuckets * 4u;
     const size_t total = sz_heads + sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     std::lock_guard<std::recursive_mutex> lk(c.mu);
     Arena &a = scratch_for(c, s).bin;
@@ -1236,6 +1236,10 @@ uint32_t val_gpu_abi_version(void) { return VAL_GPU_ABI_VERSION; }
 int vcrc_debug_times(uint64_t *out)
 {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vcrc_time), sizeof(g_vcrc_time)) == hipSuccess ? 0 : -1;
+}
+int vcrc_debug_info(uint32_t *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vcrc_info), sizeof(g_vcrc_info)) == hipSuccess ? 0 : -1;
 }
 #endif
 
