@@ -540,19 +540,24 @@ def test_wave_round_tail(vc, dev, L, extra):
     assert int(nbad.item()) == 1 and int(okh.argmin()) == bad and int(okh.sum()) == n - 1
 
 
-@pytest.mark.parametrize("strided", [True, False])
-def test_dynamic_tail_every_frame(vc, dev, strided):
+@pytest.mark.parametrize("strided,payload,per", [
+    (True, 16384, 8),    # strided groups of 8 x 16 KiB: one queue word
+    (False, 65516, 4),   # descriptor groups of 4 x 64 KiB: one queue word
+    (True, 4184, 16),    # strided groups of 16 x 4.2 KiB (67 KB): 64 queue partitions
+    (False, 4184, 16),   # descriptor groups of 16 x 4.2 KiB: 64 queue partitions
+])
+def test_dynamic_tail_every_frame(vc, dev, strided, payload, per):
     """Launches long enough for the dynamic tail (k_frames: the last half of
-    the group rounds come from a queue): 4 full rounds of the machine plus a
-    partial one, every frame checked against the oracle, then the same batch
-    again (the queue must have been re-zeroed by the previous launch)."""
+    the group rounds come from a queue, one word for long groups, 64
+    partitions for shorter ones): 4 full rounds of the machine plus a partial
+    one, every frame checked against the oracle, then the same batch again
+    (the queue must have been re-zeroed by the previous launch)."""
     vc.set_geometry()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    payload = 65516 if not strided else 16384           # descriptor groups of 4 x 64 KiB, strided 8 x 16 KiB
-    per = 4 if not strided else 8
     n = cus * 16 * per * 4 + 777
     flen = 8 + 8 + payload
     stride = flen + 4
+    assert vc.lanes_per_frame(flen) == 64 // per
     g = torch.Generator(device=dev).manual_seed(11)
     buf = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
     kw = dict(stride=stride, flen=flen, n=n) if strided else dict(

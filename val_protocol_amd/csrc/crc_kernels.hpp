@@ -39,6 +39,19 @@ __host__ __device__ inline int length_class(uint32_t L)
     return L < 1024u ? 0 : L < 8192u ? 1 : L < 49152u ? 2 : 3;
 }
 
+// Work-queue partitions: the ragged kernel's item queue (kQueueParts) and the
+// uniform kernel's dynamic tail (kDynParts), one head word each, 64 B apart;
+// the host sizes both scratch blocks from these.
+#ifndef VCRC_RAGGED_PARTS  // A/B builds may override
+#define VCRC_RAGGED_PARTS 64  // 1, 2, 4 partitions: slower (u1100 up to 2.8x); 8 -> 64: +1.5-3% (r02_ab_ragged_parts.log)
+#endif
+#ifndef VCRC_DYN_PARTS  // A/B builds may override (the host picks 1 or this per launch)
+#define VCRC_DYN_PARTS 64
+#endif
+constexpr uint32_t kQueueParts = VCRC_RAGGED_PARTS, kDynParts = VCRC_DYN_PARTS;
+static_assert(kQueueParts >= 1 && kQueueParts <= 64 && kDynParts >= 1 && kDynParts <= 64, "queue partitions");
+constexpr uint32_t kDynQueueBytes = (kDynParts + 1u) * 64u;  // heads, then the exit counter
+
 struct FrameParams {
     const uint8_t *base;
     const uint64_t *off;     // descriptor mode (NULL: strided mode)
@@ -61,8 +74,9 @@ struct FrameParams {
     uint32_t *bin_counts;    // ragged mode: k_bin_count's bucket totals, re-zeroed here for the next batch
     const uint32_t *consts;  // device constant blob (crc_device.hpp): tables and maps
     uint32_t *out_pay;       // RX by-product: raw zero-init register of each frame's payload (nullable)
-    uint32_t *qhead;         // uniform mode: dynamic-tail queue {head, exits} (zero on entry, re-zeroed), nullable
+    uint32_t *qhead;         // uniform mode: dynamic-tail queue, kDynQueueBytes (zero on entry, re-zeroed), nullable
     uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
+    uint32_t qparts;         // with qhead: queue partitions, 1..kDynParts
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -466,15 +480,20 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     }
     // Dynamic tail: the first static_rounds group rounds are dealt as above,
     // the rest are pulled one group at a time from a queue, so waves that run
-    // ahead (the oldest of a SIMD issue first) take more of the end. The last
-    // wave out re-zeroes the queue for the next launch on this stream.
+    // ahead (the oldest of a SIMD issue first) take more of the end. Short
+    // groups split the queue into P interleaved partitions (group part + P * k
+    // of the dynamic range), one head word each, keyed by blockIdx % P as in the
+    // ragged kernel (every partition has a workgroup: P <= gridDim.x); long
+    // groups keep one word, which evens the end out better. The last wave out
+    // re-zeroes the heads for the next launch on this stream.
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
     while (fb < p.n && fb < dyn) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
     for (;;) {
         uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(&p.qhead[0], 1u);
+        if (lane == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
         k = __builtin_amdgcn_readfirstlane(k);
-        const uint64_t gb = dyn + (uint64_t)k * kGroups;
+        const uint64_t gb = dyn + ((uint64_t)part + (uint64_t)P * k) * kGroups;
         if (gb >= p.n) break;
         const uint64_t fd = gb + (uint64_t)(lane / G);
         uint64_t od = 0;
@@ -484,10 +503,10 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     }
     VCRC_STAMP(2);
     if (lane == 0) {
-        const uint32_t out = atomicAdd(&p.qhead[16], 1u);
+        const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
         if (out == (uint32_t)nwaves - 1u) {  // every wave is past its last dequeue
-            atomicExch(&p.qhead[0], 0u);
-            atomicExch(&p.qhead[16], 0u);
+            for (uint32_t i = 0; i < P; i++) atomicExch(&p.qhead[i * 16u], 0u);
+            atomicExch(&p.qhead[kDynParts * 16u], 0u);
         }
     }
 }
@@ -504,13 +523,6 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 //   class 2 (G=8,  512 B rounds): L in [8192, 49152)   buckets 37..117
 //   class 3 (G=16, 1 KiB rounds): L in [49152, 65536]  buckets 118..134, longer 135
 constexpr int kBuckets = 136;
-// Work-queue partitions of the ragged kernel (one head word each, 64 B apart;
-// the host sizes the heads scratch from this).
-#ifndef VCRC_RAGGED_PARTS  // A/B builds may override
-#define VCRC_RAGGED_PARTS 64  // 1, 2, 4 partitions: slower (u1100 up to 2.8x); 8 -> 64: +1.5-3% (r02_ab_ragged_parts.log)
-#endif
-constexpr uint32_t kQueueParts = VCRC_RAGGED_PARTS;
-static_assert(kQueueParts >= 1 && kQueueParts <= 64, "queue partitions");
 __host__ __device__ inline int length_bucket(uint32_t L)
 {
     if (L < 1024u) return L <= 128u ? 0 : (int)((L - 1u) / 128u);

@@ -313,26 +313,45 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
     const int pf = prefetch_depth();
-    // dynamic tail for long launches: the last 1/8 of the group rounds (at
-    // least one) come from a queue (k_frames)
+    // Dynamic tail for long launches: the last half of the group rounds come
+    // from a queue (k_frames). Groups of >= 128 KiB (strided) or 192 KiB
+    // (descriptors) pull from one word: 4,096 waves over 128 KiB groups is
+    // about 48 dequeues/us at 6 TB/s, under the ~88/us one word serves, and
+    // one word evens the end out better than partitions (cfg3 -1.5%, cfg4 -3.7%
+    // with 64). Groups under 128 KiB pull from 64 partitions: descriptor groups
+    // from 16 KiB (u4200d +4%, u1100d +6%; with one word they lost up to 2x),
+    // strided ones from 32 KiB (s4200 +3%; s1100's 17.6 KiB groups -3%);
+    // descriptor groups of 128-192 KiB stay static (u16400d -1% either way):
+    // profiles/r02_ab_dynparts.log.
     const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * kWavesPerBlock);
     p.qhead = nullptr;
-    // a group must be long enough that the one queue word is not the limit
-    // (it serves ~88 dequeues/us): 4,096 waves over >= 128 KiB groups is
-    // about 48/us at 6 TB/s; descriptor batches, whose queued groups load
-    // their descriptors behind the dequeue, need more (u16400d: -4% at
-    // 131 KB groups; cfg4's 4 x 64 KiB groups gain)
     const uint64_t group_bytes = (uint64_t)(64 / G) * len;
-    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && group_bytes >= (p.off ? 192u << 10 : 128u << 10)) {
+#ifndef VCRC_DYN_MIN_GROUP  // A/B builds may override: one-word minimum group bytes, strided / descriptor batches
+#define VCRC_DYN_MIN_GROUP (128u << 10)
+#endif
+#ifndef VCRC_DYN_MIN_GROUP_DESC
+#define VCRC_DYN_MIN_GROUP_DESC (192u << 10)
+#endif
+#ifndef VCRC_DYN_MIN_GROUP_PARTS  // partitioned queue minimum group bytes, strided / descriptor batches
+#define VCRC_DYN_MIN_GROUP_PARTS (32u << 10)
+#endif
+#ifndef VCRC_DYN_MIN_GROUP_PARTS_DESC
+#define VCRC_DYN_MIN_GROUP_PARTS_DESC (16u << 10)
+#endif
+    const bool one_word = group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_DESC : VCRC_DYN_MIN_GROUP);
+    const bool parts =
+        group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_PARTS_DESC : VCRC_DYN_MIN_GROUP_PARTS) && group_bytes < VCRC_DYN_MIN_GROUP;
+    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
         Ctx &cm = const_cast<Ctx &>(c);
         std::lock_guard<std::recursive_mutex> lk(cm.mu);
         Arena &a = scratch_for(cm, s).queue;
         uint8_t *q = nullptr;
-        val_status_t st = arena_acquire(a, 128, s, &q);
+        val_status_t st = arena_acquire(a, kDynQueueBytes, s, &q);
         if (st != VAL_OK) return st;
-        if (!a.counts_zero) VCRC_HIP(hipMemsetAsync(q, 0, 128, s), "hipMemsetAsync(queue)");
+        if (!a.counts_zero) VCRC_HIP(hipMemsetAsync(q, 0, kDynQueueBytes, s), "hipMemsetAsync(queue)");
         a.counts_zero = true;  // the last wave out re-zeroes it
         p.qhead = reinterpret_cast<uint32_t *>(q);
+        p.qparts = one_word ? 1u : kDynParts;
 #ifndef VCRC_DYN_DIV
 #define VCRC_DYN_DIV 2
 #endif
