@@ -489,20 +489,24 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
     while (fb < p.n && fb < dyn) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
     const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
+    // the lane id again from mbcnt: kept live from the entry, it was the one
+    // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
+    // launch later)
+    const int ql = (int)__lane_id();
     for (;;) {
         uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
+        if (ql == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
         k = __builtin_amdgcn_readfirstlane(k);
         const uint64_t gb = dyn + ((uint64_t)part + (uint64_t)P * k) * kGroups;
         if (gb >= p.n) break;
-        const uint64_t fd = gb + (uint64_t)(lane / G);
+        const uint64_t fd = gb + (uint64_t)(ql / G);
         uint64_t od = 0;
         uint32_t Ld = 0;
         if (fd < p.n) frame_desc(p, fd, od, Ld);
-        hash_frame<G, PF, PAY, false>(p, fd, fd < p.n, od, Ld, lane % G, sb, G, [] {});
+        hash_frame<G, PF, PAY, false>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
     }
     VCRC_STAMP(2);
-    if (lane == 0) {
+    if (ql == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
         if (out == (uint32_t)nwaves - 1u) {  // every wave is past its last dequeue
             for (uint32_t i = 0; i < P; i++) atomicExch(&p.qhead[i * 16u], 0u);
