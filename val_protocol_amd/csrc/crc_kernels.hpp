@@ -77,6 +77,7 @@ struct FrameParams {
     uint32_t *qhead;         // uniform mode: dynamic-tail queue, kDynQueueBytes (zero on entry, re-zeroed), nullable
     uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
     uint32_t qparts;         // with qhead: queue partitions, 1..kDynParts
+    uint32_t r0x4;           // uniform batches: whole round-0 units by dwordx4 (load_unit0)
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -122,14 +123,19 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
 // BF (k_region): branch-free, every lane issues the loads.
 // Otherwise (k_frames): only lanes with a unit issue them; measured faster on
 // frame batches (the dummy loads cost cfg2 3%, a 256-frame window 9%).
+// r0x4 (k_frames, uniform batches whose round 0 is at least half full): the
+// lanes holding a whole unit read it by dwordx4 as in k_region (2048 x 64 KiB
+// windows 39.7 -> 35.6 us; cfg2, whose round 0 holds unit 0 alone, -1.3% with
+// it: profiles/r02_ab_r0x4.log).
 template <bool BF>
-__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad, gu8 *dummy)
+__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad, gu8 *dummy,
+                                           bool r0x4)
 {
     const bool has = u >= 0 && Lg >= 4;
     if (BF || has) {
         gu8 *base = has ? fp + ((int64_t)u * kUnit - pad) : dummy;
         const uint32_t lo = (has && u == 0) ? (pad & ~3u) : 0u;
-        if (BF && lo == 0) {
+        if (lo == 0 && (BF || (r0x4 && u > 0))) {
             // k_region: every unit but the window's first is whole, so four
             // dwordx4 loads instead of sixteen dword loads: 8 MiB windows
             // 15.9 -> 10.9 us. In k_frames round 0 mostly holds unit 0 alone
@@ -248,7 +254,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     uint32_t w0[kWords];
     const bool tiny = u0 == 0 && Lg < 4;
     gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
-    load_unit0<BF>(w0, u0, fp, Lg, pad, dummy);
+    load_unit0<BF>(w0, u0, fp, Lg, pad, dummy, p.r0x4 != 0);
     // header_crc: by the lane holding unit 0, from the frame's first line,
     // which round 0 reads anyway (read after the merge, the line had left the
     // caches: +0.4% HBM traffic on cfg3).

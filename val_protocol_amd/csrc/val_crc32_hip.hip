@@ -357,6 +357,11 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
 #endif
         p.static_rounds = (uint32_t)(VCRC_DYN_DIV == 1 ? 1u : rounds - std::max<uint64_t>(1, rounds / VCRC_DYN_DIV));
     }
+    {  // round 0 of a typical frame at least half full: its whole units by dwordx4
+        const uint64_t U = std::max<uint64_t>(1, ((uint64_t)len + kUnit - 1) / kUnit);
+        const uint64_t r0 = U - (uint64_t)G * ((U + G - 1) / G - 1);
+        p.r0x4 = r0 * 2 >= G ? 1u : 0u;
+    }
     switch (G) {
     case 1: launch_uniform_g<1>(pf, grid, s, p); break;
     case 2: launch_uniform_g<2>(pf, grid, s, p); break;
