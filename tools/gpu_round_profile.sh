@@ -15,8 +15,8 @@ timeout -k 10 600 python bench.py --config cfg2 --no-cpu-baseline --steps 200 > 
 timeout -k 10 600 python bench.py --config cfg5 --no-cpu-baseline > $O/bench_cfg5.json 2> $O/bench_cfg5.err && \
 timeout -k 10 600 python tools/host_inclusive.py > $O/host_inclusive.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 $R/bench.py --steps 10 --no-cpu-baseline > $O/trace.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace5 -o bench -- python3 $R/bench.py --config cfg5 --steps 10 --no-cpu-baseline > $O/trace5.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- python3 $R/bench.py --no-cpu-baseline > $O/trace.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace5 -o bench -- python3 $R/bench.py --config cfg5 --no-cpu-baseline > $O/trace5.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_v -o p -- python3 $R/tools/prof_target.py cfg3 3 verify > $O/pmc_fetch_v.log 2>&1 && \

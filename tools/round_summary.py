@@ -62,9 +62,11 @@ def kernel_trace(o, sub, rnd, tag):
             w.writerow([r["Dispatch_Id"], r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"])])
     top = max(csv.DictReader(open(stats)), key=lambda r: float(r["TotalDurationNs"]))
     main = [r for r in crc if r["Kernel_Name"] == top["Name"]]
-    last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in main[-10:]]
+    steps = int(os.environ.get("BENCH_STEPS", "20"))  # bench.py's timed steps (default 20, after 15 warmup)
+    last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in main[-steps:]]
     return {"kernel": top["Name"], "dispatches": int(top["Calls"]), "avg_ms_all_dispatches": float(top["AverageNs"]) / 1e6,
-            "avg_ms_timed_region_last10": sum(last) / len(last) / 1e6 if last else None}
+            "timed_dispatches": len(last),
+            "avg_ms_timed_region": sum(last) / len(last) / 1e6 if last else None}
 
 
 def main():
