@@ -92,14 +92,17 @@ def main():
             for i, l in enumerate(libs):
                 vc._lib = l
                 out = torch.empty(w.get("n") or w["length"].numel(), dtype=torch.int32, device=dev)
+                hdr = torch.empty_like(out) if os.environ.get("AB_HDR") == "1" else None  # header_crc too
                 if "off" in w:
-                    fn = lambda: vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, len_hint=w["len_hint"])
+                    fn = lambda: vc.frames(w["buf"], off=w["off"], length=w["length"], out_crc=out, out_hdr=hdr,
+                                           len_hint=w["len_hint"])
                 else:
-                    fn = lambda: vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out)
+                    fn = lambda: vc.frames(w["buf"], stride=w["stride"], flen=w["flen"], n=w["n"], out_crc=out,
+                                           out_hdr=hdr)
                 med, _ = time_it(fn, reps=10)
                 res[i].append(med)
                 if rep == 0:
-                    outs.append(out.clone())
+                    outs.append(out.clone() if hdr is None else torch.cat([out, hdr]))
         a = np.median(res[0])
         line = f"{name}: A {a:.4f} ms ({nbytes / a / 1e6:.0f} GB/s)"
         for i in range(1, len(libs)):
