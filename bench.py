@@ -115,12 +115,15 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(sample: np.ndarray, n: int, threads: int, stride: int = 0, flen: int = 0, off=None, length=None):
+def cpu_baseline(sample: np.ndarray, n: int, threads: int, stride: int = 0, flen: int = 0, off=None, length=None,
+                 all_threads: int = 0):
     """Time the reference's own val_crc32 (oracle/_ref/libref_bench.so, built
     from /root/reference/src/val_core.c:150-160) -- or the oracle port if that
     build is absent -- over a host copy of `n` frames of the same workload:
-    once on 1 thread and once on `threads` threads (frames round-robin).
-    Returns (GiB/s at `threads`, GiB/s on 1 thread, kind, outputs, detail)."""
+    on 1 thread, on `threads` threads and on `all_threads` (every core this
+    process may run on; frames round-robin over pthreads).
+    Returns (GiB/s at `threads`, GiB/s on 1 thread, kind, outputs, detail,
+    GiB/s on all_threads)."""
     kind = "reference"
     so = os.path.join(ROOT, "oracle", "_ref", "libref_bench.so")
     out = np.zeros(n, np.uint32)
@@ -166,7 +169,9 @@ def cpu_baseline(sample: np.ndarray, n: int, threads: int, stride: int = 0, flen
 
     one, reps1 = rate(1, 3.0, 3.0)
     many, reps = rate(threads, 10.0, 4.0)
-    return many, one, kind, out, f"x{reps} reps on {threads} threads, x{reps1} on 1 thread"
+    allc, repsa = rate(all_threads, 10.0, 4.0) if all_threads and all_threads != threads else (many, reps)
+    return (many, one, kind, out, f"x{reps} reps on {threads} threads, x{repsa} on {all_threads or threads}, "
+            f"x{reps1} on 1 thread", allc)
 
 
 def read_pmc_traffic(config: str):
@@ -315,6 +320,8 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
+    # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
+    bytes_per_launch = int(d_len.long().sum().item()) if desc else n * flen
 
     # Parity spot check of this run's output against the oracle (not timed).
     sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, 256, replace=False), [0, n - 1]]))
@@ -334,9 +341,19 @@ def main():
     parity = bool(np.array_equal(got, want))
     if args.verify:
         parity = parity and int(nbad.item()) == 0
+    # Per-rank record (BASELINE configs[3]: "per-GPU and aggregate GiB/s"):
+    # each rank's own frames, kernel time by events and wall time between the
+    # barriers; gathered on rank 0 (the only other collective of the run).
+    mine = {"rank": rank, "device": gpu, "frames": n, "bytes_per_step": bytes_per_launch,
+            "kernel_ms": round(kern_ms, 4), "elapsed_s": round(elapsed, 6),
+            "GiB_s": round(bytes_per_launch * args.steps / elapsed / GIB, 2),
+            "kernel_GiB_s": round(bytes_per_launch / (kern_ms * 1e-3) / GIB, 2), "parity_sample_ok": parity,
+            "last_frame_crc_input": int(d_len[n - 1].item()) if desc and n else flen}
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
-    # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
-    bytes_per_launch = int(d_len.long().sum().item()) if desc else n * flen
     file_crc_input = (n_total - 1) * flen + 8 + (CFG4_FILE - (n_total - 1) * payload) + (8 if explicit else 0)
     total_bytes = (file_crc_input if strong else bytes_per_launch * world) * args.steps
     value = total_bytes / elapsed_max / GIB
@@ -383,6 +400,7 @@ def main():
         except AttributeError:
             avail = os.cpu_count() or 1
         threads = args.cpu_threads or min(16, avail)  # the GPU box's CPU share is 16 per GPU
+        all_threads = avail  # also N = all host cores visible to this process
         if ragged:
             offs_all = d_off.cpu().numpy()
             lens_all = d_len.cpu().numpy().astype(np.uint32)
@@ -390,17 +408,19 @@ def main():
             ns = int(np.searchsorted(ends, 1 << 30, side="right"))  # ~1 GiB of the batch
             ns = max(1, min(ns, n))
             host_rows = flat[: int(ends[ns - 1])].cpu().numpy()
-            cgibs, one, kind, cout, detail = cpu_baseline(host_rows, ns, threads, off=offs_all[:ns],
-                                                          length=lens_all[:ns])
+            cgibs, one, kind, cout, detail, call = cpu_baseline(host_rows, ns, threads, off=offs_all[:ns],
+                                                                length=lens_all[:ns], all_threads=all_threads)
             sample_bytes = int(lens_all[:ns].astype(np.int64).sum())
         else:
             ns = min(n, max(1, (1 << 30) // flen))  # ~1 GiB host sample of the same frames
             host_rows = buf[:ns].cpu().numpy().reshape(-1)
-            cgibs, one, kind, cout, detail = cpu_baseline(host_rows, ns, threads, stride=stride, flen=flen)
+            cgibs, one, kind, cout, detail, call = cpu_baseline(host_rows, ns, threads, stride=stride, flen=flen,
+                                                                all_threads=all_threads)
             sample_bytes = ns * flen
         same = bool(np.array_equal(cout, crc[:ns].cpu().numpy().view(np.uint32))) if not args.verify else None
         cpu = {"value": round(cgibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-               "value_1core": round(one, 3), "cpu_model": cpu_model(), "cores_visible": avail,
+               "value_1core": round(one, 3), "value_all_cores": round(call, 3), "cores_all": all_threads,
+               "cpu_model": cpu_model(), "cores_visible": avail,
                "sample": f"first {ns} frames of this batch ({sample_bytes / GIB:.2f} GiB of CRC input), "
                          f"reference val_crc32 per frame (src/val_core.c:150-160), frames round-robin over "
                          f"pthreads, {detail}; outputs equal GPU: {same}"}
@@ -453,6 +473,12 @@ def main():
                 "frac_of_read_roof": round(achieved_gbs / roof, 4) if roof else None,
             },
             "cpu_baseline": cpu,
+            # per-GPU rates and the aggregate's denominator (BASELINE configs[3])
+            "per_rank": per_rank,
+            "aggregate_over_max_rank": {
+                "total_bytes": total_bytes, "max_elapsed_s": round(elapsed_max, 6),
+                "slowest_rank": max(per_rank, key=lambda r: r["elapsed_s"])["rank"],
+                "sum_of_rank_GiB_s": round(sum(r["GiB_s"] for r in per_rank), 2)},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

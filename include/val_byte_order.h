@@ -8,6 +8,15 @@
 #define VAL_BYTE_ORDER_H
 #include <stdint.h>
 
+/* forced inlining for the small helpers of VAL's own sources */
+#ifndef VAL_FORCE_INLINE
+#if defined(__GNUC__) || defined(__clang__)
+#define VAL_FORCE_INLINE inline __attribute__((always_inline))
+#else
+#define VAL_FORCE_INLINE inline
+#endif
+#endif
+
 static inline void val_put_le16(uint8_t *p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
 static inline void val_put_le32(uint8_t *p, uint32_t v)
 {

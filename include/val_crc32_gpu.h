@@ -29,13 +29,16 @@
  *                              (a window of src/val_sender.c:
  *                              822-841 sharded by contiguous frame ranges)
  *
- * Every entry point computes on the GPU. Batch calls return VAL_ERR_IO on a
- * missing device or a HIP failure. The three scalar hooks (provider,
- * val_crc32, val_crc32_update_state) have no error channel and are called by
- * VAL under its session mutex on every frame, so on a GPU failure they return
- * the CRC from this library's own CPU slice-by-8 and count it
- * (val_gpu_cpu_fallback_count); VAL_GPU_CPU_FALLBACK=0 or
- * val_gpu_set_cpu_fallback(0) makes them abort instead.
+ * Batch, region and device calls compute on the GPU only and return
+ * VAL_ERR_IO on a missing device or a HIP failure. The three scalar hooks
+ * (provider, val_crc32, val_crc32_update_state) take host memory, have no
+ * error channel and are called by VAL under its session mutex on every
+ * frame: inputs below the provider threshold (val_gpu_provider_min_bytes)
+ * are answered by this library's own CPU engine, where a GPU round trip
+ * cannot win, so the drop-in is never slower than the reference's byte loop;
+ * longer inputs run on the GPU. On a GPU failure the hooks return the CRC
+ * from the same CPU engine and count it (val_gpu_cpu_fallback_count);
+ * VAL_GPU_CPU_FALLBACK=0 or val_gpu_set_cpu_fallback(0) makes them abort.
  */
 #ifndef VAL_CRC32_GPU_H
 #define VAL_CRC32_GPU_H
@@ -79,6 +82,27 @@ void val_gpu_set_cpu_fallback(int enable);
 
 /* ---- scalar hooks (host memory) --------------------------------------- */
 uint32_t val_gpu_crc32_provider(uint32_t seed, const void *buf, size_t len);
+/* Inputs shorter than this many bytes are answered on the CPU by the scalar
+ * hooks (the measured crossover). Set with
+ * val_gpu_set_provider_min_bytes (-1 = VAL_GPU_PROVIDER_MIN_BYTES from the
+ * environment, else the built-in default; 0 = always the GPU). */
+void val_gpu_set_provider_min_bytes(int64_t bytes);
+uint64_t val_gpu_provider_min_bytes(void);
+/* Scalar-hook calls answered on the CPU because they were below the threshold. */
+uint64_t val_gpu_cpu_small_count(void);
+/* Where the calling thread's last scalar-hook call was answered. */
+#define VAL_GPU_HOOK_NONE 0     /* no call yet on this thread */
+#define VAL_GPU_HOOK_GPU 1      /* on the GPU */
+#define VAL_GPU_HOOK_CPU 2      /* on the CPU, below the threshold */
+#define VAL_GPU_HOOK_FALLBACK 3 /* on the CPU after the GPU path failed */
+int val_gpu_last_hook_path(void);
+/* The library's CPU engine itself: raw register after feeding data[0, len)
+ * to state (val_crc32_update_state semantics). engine: 0 = the best this CPU
+ * has, 1 = slice-by-16, 2 = carry-less multiply (PCLMULQDQ), 3 = 512-bit
+ * carry-less multiply (VPCLMULQDQ + AVX-512); an engine the CPU lacks runs
+ * the next simpler one. val_crc32_cpu_engine() = the engine 0 selects. */
+uint32_t val_crc32_cpu_update_state(uint32_t state, const void *data, size_t len, int engine);
+int val_crc32_cpu_engine(void);
 uint32_t val_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 /* state * x^(8*nbytes) mod P: advance a raw register over nbytes zero bytes. */
 uint32_t val_crc32_shift(uint32_t state, uint64_t nbytes);
@@ -125,8 +149,10 @@ val_status_t val_crc32_verify_frames_ex_dev(const uint8_t *d_base, const uint64_
  * finalize with ^0xFFFFFFFF). One launch at any length: windows up to 8
  * KiB are one 64-lane frame; longer ones are chunked over the whole machine
  * and folded inside the same launch through a 128-byte library-owned device
- * accumulator, which calls on different streams share in turn (each call's
- * stream waits on the previous user's completion event). */
+ * accumulator kept per stream (calls on one stream are ordered by it; calls
+ * on different streams use different accumulators; hipStreamPerThread is
+ * keyed per calling thread). The call runs on the stream's device (else the
+ * device d_ptr lives on). */
 val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t state_in, uint32_t *d_state_out,
                                   void *stream);
 /* Scratch bytes the region call needs for a given length (informational). */
@@ -139,7 +165,7 @@ uint64_t val_crc32_region_scratch_bytes(uint64_t len);
  * previous chunk is hashed (descriptor batches chunk when their offsets are
  * non-decreasing). A pinned `base` (val_gpu_host_alloc, hipHostMalloc or
  * hipHostRegister) is copied by DMA in place; pageable memory goes through
- * two internal pinned bounce buffers (host memcpy, up to 8 threads).
+ * two internal pinned bounce buffers (host memcpy, val_gpu_host_copy_threads).
  * Mixed-length descriptor batches take the device-binned ragged path.   */
 val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                                    uint64_t stride, uint32_t flen, uint32_t n, uint32_t *crc, uint32_t *hdr);
@@ -155,9 +181,23 @@ val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_
  * first frame with ok[i] == 0 (ok nullable = all): for each frame
  * state = shift(state, pay_len[i]) ^ pay_state[i], i.e.
  * val_crc32_update_state(state, payload_i) without touching the bytes again.
- * *n_folded (nullable) = frames folded. Host only (no GPU call). */
+ * The caller passes only in-order DATA frames (each payload starts where the
+ * previous one ended); for a window that may hold duplicates, gaps or control
+ * frames use val_crc32_fold_payload_states_at. *n_folded (nullable) = frames
+ * folded. Host only (no GPU call). */
 uint32_t val_crc32_fold_payload_states(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len,
                                        const uint8_t *ok, uint32_t n, uint32_t *n_folded);
+/* The same fold with the receiver's ordering rule (reference
+ * src/val_receiver.c:871-891): file_off[i] from val_frame_data_offsets
+ * (val_wire.h). A frame is folded, and *written advanced by its payload,
+ * only when it is a DATA frame with ok[i] != 0 whose effective offset
+ * (file_off[i], or *written for VAL_FRAME_OFFSET_IMPLIED) equals *written;
+ * duplicates (earlier offsets) and gaps (later ones) are skipped and the
+ * frames after them are still judged one by one, as the receiver does.
+ * *n_folded (nullable) = frames folded. Host only. */
+uint32_t val_crc32_fold_payload_states_at(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len,
+                                          const uint64_t *file_off, const uint8_t *ok, uint32_t n, uint64_t *written,
+                                          uint32_t *n_folded);
 
 /* ---- several GPUs in one process ----------------------------------------
  * The *_host batches above split into ndev shards (ndev <= 0: one per
@@ -193,10 +233,22 @@ uint32_t val_crc32_fold_partials(const uint32_t *state, const uint64_t *nbytes, 
  * without a bounce. NULL on failure (val_gpu_last_error). */
 void *val_gpu_host_alloc(size_t bytes);
 void val_gpu_host_free(void *p);
+/* Host threads one pageable-to-pinned copy of `bytes` uses when
+ * `concurrent_copies` run at once (one per device in the *_host_multi
+ * calls): one per 4 MiB, at most 8, and all copies together within the
+ * process's CPU affinity set. */
+uint32_t val_gpu_host_copy_threads(uint64_t bytes, uint32_t concurrent_copies);
 /* Wire bytes per H2D chunk of the *_frames_host calls; 0 = default (64 MiB).
  * Device memory use is two chunks. Speed and memory only; results never change. */
 val_status_t val_gpu_set_host_chunk_bytes(size_t bytes);
 
+/* ---- build and introspection --------------------------------------------
+ * Diagnostic compile-time switches this library was built with, as a
+ * space-separated list ("" for a product build). Switches that change
+ * results can only be enabled in a VCRC_DIAG_BUILD, and such a build reports
+ * "VCRC_DIAG_BUILD" here; tests/test_build.py asserts the in-tree library
+ * reports nothing. */
+const char *val_gpu_build_flags(void);
 /* ---- introspection for benchmarks ---------------------------------------
  * Lanes per frame the library would pick for a given typical length. */
 uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);

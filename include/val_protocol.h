@@ -13,8 +13,11 @@
  *      tests/test_abi.py against the reference's own layout)
  *   - val_crc32                   reference include/val_protocol.h:377
  * Session, transport, filesystem and flow-control *behaviour* stays in the
- * reference's control plane; only their types are declared here so the
- * config layout matches.
+ * reference's control plane. Its public surface is declared here unchanged
+ * (types, constants, the session API of reference :363-446), so the
+ * reference's own src/val_core.c, val_sender.c, val_receiver.c and
+ * val_wire.c compile against these headers (tests/test_header_surface.py)
+ * and link against this library's val_crc32* / provider.
  */
 #ifndef VAL_PROTOCOL_H
 #define VAL_PROTOCOL_H
@@ -55,6 +58,9 @@ typedef enum {
     VAL_PKT_DATA_NAK = 13
 } val_packet_type_t;
 
+/* DATA_ACK payload flags (reserved by v0.7) */
+typedef enum { VAL_ACK_FLAG_HEARTBEAT = 1u << 0, VAL_ACK_FLAG_EOF = 1u << 1 } val_ack_flags_t;
+
 /*
  * CRC-32 provider hook. Semantics fixed by the reference's call sites
  * (src/val_core.c:399-406, :431-438), which always pass seed = 0xFFFFFFFF and
@@ -85,6 +91,35 @@ typedef struct {
 } val_memory_allocator_t;
 
 typedef enum { VAL_RESUME_NEVER = 0, VAL_RESUME_SKIP_EXISTING = 1, VAL_RESUME_TAIL = 2 } val_resume_mode_t;
+
+/* Receiver's answer to RESUME_REQ (wire form: val_serialize_resume_resp). */
+typedef enum {
+    VAL_RESUME_START_ZERO = 0,
+    VAL_RESUME_START_OFFSET = 1,
+    VAL_RESUME_VERIFY_FIRST = 2,
+    VAL_RESUME_SKIP_FILE = 3,
+    VAL_RESUME_ABORT_FILE = 4
+} val_resume_action_t;
+
+typedef struct {
+    val_resume_action_t action;
+    uint64_t resume_offset;
+    uint32_t verify_crc;    /* CRC-32 of the verify window: the region CRC (val_crc32_region_dev) */
+    uint64_t verify_length;
+} val_resume_resp_t;
+
+typedef enum {
+    VAL_LOG_OFF = 0,
+    VAL_LOG_CRITICAL = 1,
+    VAL_LOG_WARNING = 2,
+    VAL_LOG_INFO = 3,
+    VAL_LOG_DEBUG = 4,
+    VAL_LOG_TRACE = 5
+} val_log_level_t;
+
+/* Optional features negotiated in the handshake: none are defined in v0.7. */
+#define VAL_FEAT_NONE 0u
+#define VAL_BUILTIN_FEATURES VAL_FEAT_NONE
 
 typedef struct {
     val_resume_mode_t mode;
@@ -192,8 +227,56 @@ typedef struct {
     } capture;
 } val_config_t;
 
-/* CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init and xorout 0xFFFFFFFF),
- * computed by the MI355X kernels (see val_crc32_gpu.h for the batch forms). */
+/* ---- session API (implemented by the reference's control plane, which
+ * this library does not replace; declared so its sources build here) ---- */
+/* control-plane API begin */
+val_status_t val_session_create(const val_config_t *config, val_session_t **out_session, uint32_t *out_detail);
+void val_session_destroy(val_session_t *session);
+val_status_t val_send_files(val_session_t *session, const char *const *filepaths, size_t file_count,
+                            const char *sender_path);
+val_status_t val_receive_files(val_session_t *session, const char *output_directory);
+void val_clean_filename(const char *input, char *output, size_t output_size);
+void val_clean_path(const char *input, char *output, size_t output_size);
+val_status_t val_get_cwnd_packets(val_session_t *session, uint32_t *out_cwnd);
+val_status_t val_get_peer_tx_cap_packets(val_session_t *session, uint32_t *out_cap);
+val_status_t val_get_effective_packet_size(val_session_t *session, size_t *out_packet_size);
+uint32_t val_get_builtin_features(void);
+val_status_t val_get_last_error(val_session_t *session, val_status_t *code, uint32_t *detail_mask);
+val_status_t val_get_error(val_session_t *session, val_error_t *out);
+val_status_t val_emergency_cancel(val_session_t *session);
+bool val_check_for_cancel(val_session_t *session);
+void val_config_validation_disabled(val_config_t *config);
+void val_config_set_validator(val_config_t *config, val_metadata_validator_t validator, void *context);
+
+#if VAL_ENABLE_METRICS
+/* Per-session counters (reference builds with VAL_ENABLE_METRICS=1);
+ * crc_errors is what val_crc32_verify_frames_* count per batch. */
+typedef struct {
+    uint64_t packets_sent;
+    uint64_t packets_recv;
+    uint64_t bytes_sent;
+    uint64_t bytes_recv;
+    uint64_t send_by_type[32]; /* by on-wire type byte, CANCEL (0x18) included */
+    uint64_t recv_by_type[32];
+    uint32_t timeouts;
+    uint32_t timeouts_hard;
+    uint32_t retransmits;
+    uint32_t crc_errors;
+    uint32_t handshakes;
+    uint32_t files_sent;
+    uint32_t files_recv;
+    uint32_t rtt_samples;
+} val_metrics_t;
+val_status_t val_get_metrics(val_session_t *session, val_metrics_t *out);
+val_status_t val_reset_metrics(val_session_t *session);
+#endif
+/* control-plane API end */
+
+/* ---- CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init and xorout
+ * 0xFFFFFFFF): implemented by this library (val_crc32_gpu.h has the batch
+ * forms and the provider). val_crc32 is the reference's public utility
+ * (:377); the state functions are its internal incremental API
+ * (src/val_internal.h:628-641). */
 uint32_t val_crc32(const void *data, size_t length);
 uint32_t val_crc32_init_state(void);
 uint32_t val_crc32_update_state(uint32_t state, const void *data, size_t length);

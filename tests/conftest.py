@@ -7,6 +7,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# The scalar hooks answer inputs below the provider threshold on the CPU by
+# design. The suite sets the threshold to 0 before the library loads, so
+# every hook call a GPU test checks runs on the GPU (child processes inherit
+# it); tests of the CPU engine set it explicitly (val_gpu_set_provider_min_bytes).
+os.environ["VAL_GPU_PROVIDER_MIN_BYTES"] = "0"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C ABI)")
@@ -35,6 +41,7 @@ def _gpu_results_came_from_the_gpu(request):
         return
     import val_protocol_amd.crc as vc
 
-    before = vc.cpu_fallback_count()
+    before = vc.cpu_fallback_count(), vc.cpu_small_count()
     yield
-    assert vc.cpu_fallback_count() == before, "a scalar hook fell back to the CPU during a GPU test"
+    assert vc.cpu_fallback_count() == before[0], "a scalar hook fell back to the CPU during a GPU test"
+    assert vc.cpu_small_count() == before[1], "a scalar hook answered below the threshold during a GPU test"

@@ -19,6 +19,8 @@ def _declared_functions():
     names = set()
     for h in ("val_crc32_gpu.h", "val_protocol.h", "val_wire.h"):
         txt = open(os.path.join(INC, h)).read()
+        # the session API is the reference's control plane, declared for its sources, not exported here
+        txt = re.sub(r"/\* control-plane API begin \*/.*?/\* control-plane API end \*/", "", txt, flags=re.S)
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         txt = re.sub(r"static inline[^{]*\{[^}]*\}", "", txt)
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*\b(val_[a-z0-9_]+)\s*\(", txt, re.M):

@@ -31,3 +31,22 @@ def test_in_tree_library_is_current():
     rebuilds it under a lock otherwise."""
     _build.ensure_built()
     assert _build.is_current()
+
+
+def test_shipped_library_is_a_product_build():
+    """No diagnostic switch is compiled into the in-tree library (those that
+    change results cannot even compile without VCRC_DIAG_BUILD)."""
+    import val_protocol_amd.crc as vc
+
+    assert vc.build_flags() == ""
+
+
+def test_wrong_result_switches_need_a_diag_build():
+    import shutil
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    src = os.path.join(_build.CSRC, "val_crc32_hip.hip")
+    for flag in ("-DVCRC_DIAG_NOHASH", "-DVCRC_NO_LDS_FILL", "-DVCRC_REGION_HASHONLY", "-DVCRC_REGION_NOATOMIC"):
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", flag, f"-I{_build.INC}",
+                            f"-I{_build.CSRC}", src], capture_output=True, text=True)
+        assert r.returncode != 0 and "VCRC_DIAG_BUILD" in r.stderr, flag

@@ -48,6 +48,13 @@ def test_bench_two_ranks_weak_cfg2():
     assert line["config"]["parity_sample_ok"] is True
     assert line["config"]["frames_per_gpu"] == 65536
     assert line["value"] > 0 and line["cpu_baseline"] is None
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert all(r["frames"] == 65536 and r["parity_sample_ok"] and r["GiB_s"] > 0 and r["kernel_ms"] > 0 for r in pr)
+    agg = line["aggregate_over_max_rank"]
+    assert agg["max_elapsed_s"] == max(r["elapsed_s"] for r in pr)
+    assert agg["total_bytes"] == 2 * 2 * 65536 * (8 + 8 + 1024)  # 2 ranks x 2 steps
+    assert abs(line["value"] - agg["total_bytes"] / agg["max_elapsed_s"] / 2**30) / line["value"] < 0.01
 
 
 def test_bench_two_ranks_strong_cfg4():
@@ -56,6 +63,10 @@ def test_bench_two_ranks_strong_cfg4():
     assert line["config"]["parity_sample_ok"] is True
     assert line["config"]["frames_total"] == 131113
     assert line["config"]["frames_per_gpu"] in (65556, 65557)  # rank 0's byte-balanced share
+    pr = line["per_rank"]
+    assert sum(r["frames"] for r in pr) == 131113 and all(r["parity_sample_ok"] for r in pr)
+    # the file's 800-B remainder is the last rank's last frame; every other frame is a full one
+    assert pr[-1]["last_frame_crc_input"] == 8 + 8 + 800 and pr[0]["last_frame_crc_input"] == 8 + 8 + 65516
 
 
 def _region_worker(rank, world, port, data, q):

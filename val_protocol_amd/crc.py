@@ -12,8 +12,11 @@ in ``include/val_crc32_gpu.h``). Names mirror the reference interface:
   frames (reference ``src/val_core.c:828-834`` and ``:963-974``)
 * ``region`` -- long-window CRC (reference ``src/val_core.c:414-455``)
 
-Every call computes on the GPU. If the shared library is missing or the GPU
-path fails, calls raise; there is no CPU fallback.
+Batch, region and device calls compute on the GPU; if the shared library is
+missing or the GPU path fails, calls raise (no CPU fallback). The scalar
+hooks answer inputs below the provider threshold with the library's own CPU
+engine by design (``provider_min_bytes``; 0 forces the GPU) and raise if
+the GPU path failed.
 """
 from __future__ import annotations
 
@@ -47,8 +50,18 @@ EXPORTS = (
     "val_gpu_cpu_fallback_count", "val_gpu_set_cpu_fallback", "val_crc32_frames_host_multi",
     "val_crc32_verify_frames_host_multi", "val_crc32_region_host_multi", "val_shard_frames", "val_crc32_fold_partials",
     "val_crc32_verify_frames_ex_dev", "val_crc32_verify_frames_ex_host", "val_crc32_fold_payload_states",
-    "val_frame_payload_lens",
+    "val_frame_payload_lens", "val_gpu_set_provider_min_bytes", "val_gpu_provider_min_bytes",
+    "val_gpu_cpu_small_count", "val_gpu_last_hook_path", "val_crc32_cpu_update_state", "val_crc32_cpu_engine",
+    "val_crc32_fold_payload_states_at", "val_frame_data_offsets", "val_gpu_build_flags",
+    "val_gpu_host_copy_threads",
+    "val_serialize_handshake", "val_deserialize_handshake", "val_serialize_meta", "val_deserialize_meta",
+    "val_serialize_resume_resp", "val_deserialize_resume_resp", "val_serialize_verify_request",
+    "val_deserialize_verify_request", "val_serialize_verify_response", "val_deserialize_verify_response",
+    "val_serialize_error_payload", "val_deserialize_error_payload",
 )
+
+# Where the calling thread's last scalar-hook call was answered (val_gpu_last_hook_path).
+HOOK_NONE, HOOK_GPU, HOOK_CPU, HOOK_FALLBACK = 0, 1, 2, 3
 
 
 class ValError(RuntimeError):
@@ -115,6 +128,17 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_crc32_verify_frames_ex_host", i32, _vp, u64, _vp, _vp, u64, u32, u32, _vp, _vp, _vp)
     fn("val_crc32_fold_payload_states", u32, u32, _vp, _vp, _vp, u32, ctypes.POINTER(u32))
     fn("val_frame_payload_lens", None, _vp, _vp, _vp, u32, _vp)
+    fn("val_gpu_set_provider_min_bytes", None, ctypes.c_int64)
+    fn("val_gpu_provider_min_bytes", u64)
+    fn("val_gpu_cpu_small_count", u64)
+    fn("val_gpu_last_hook_path", ctypes.c_int)
+    fn("val_crc32_cpu_update_state", u32, u32, _vp, sz, ctypes.c_int)
+    fn("val_crc32_cpu_engine", ctypes.c_int)
+    fn("val_crc32_fold_payload_states_at", u32, u32, _vp, _vp, _vp, _vp, u32, ctypes.POINTER(u64),
+       ctypes.POINTER(u32))
+    fn("val_frame_data_offsets", None, _vp, _vp, _vp, u32, _vp)
+    fn("val_gpu_build_flags", ctypes.c_char_p)
+    fn("val_gpu_host_copy_threads", u32, u64, u32)
 
 
 def lib() -> ctypes.CDLL:
@@ -187,13 +211,49 @@ def cpu_fallback_count() -> int:
     return int(lib().val_gpu_cpu_fallback_count())
 
 
+def cpu_small_count() -> int:
+    """Scalar-hook calls answered on the CPU because they were below the provider threshold."""
+    return int(lib().val_gpu_cpu_small_count())
+
+
+def last_hook_path() -> int:
+    """HOOK_GPU / HOOK_CPU / HOOK_FALLBACK: where this thread's last scalar-hook call ran."""
+    return int(lib().val_gpu_last_hook_path())
+
+
+def set_provider_min_bytes(nbytes: int) -> None:
+    """Scalar hooks answer inputs shorter than nbytes on the CPU (0: always the
+    GPU; -1: VAL_GPU_PROVIDER_MIN_BYTES or the built-in crossover)."""
+    lib().val_gpu_set_provider_min_bytes(int(nbytes))
+
+
+def provider_min_bytes() -> int:
+    return int(lib().val_gpu_provider_min_bytes())
+
+
+def cpu_update_state(state: int, data, engine: int = 0) -> int:
+    """The library's CPU engine (0 best, 1 slice-by-16, 2 PCLMULQDQ, 3 VPCLMULQDQ)."""
+    p, n, keep = _buf(data)
+    return int(lib().val_crc32_cpu_update_state(state & 0xFFFFFFFF, p, n, engine))
+
+
+def cpu_engine() -> int:
+    return int(lib().val_crc32_cpu_engine())
+
+
+def build_flags() -> str:
+    """Compile-time switches of the loaded library ("" for a product build)."""
+    return lib().val_gpu_build_flags().decode()
+
+
 def _scalar(fn, *args) -> int:
-    """Call a scalar hook and fail loudly if it did not run on the GPU (the C
-    hooks fall back to the CPU because crc32_func_t has no error channel; this
-    Python API has one)."""
-    before = cpu_fallback_count()
+    """Call a scalar hook and fail loudly if the GPU path failed (the C hooks
+    then fall back to the CPU because crc32_func_t has no error channel; this
+    Python API has one). Inputs below the provider threshold are answered on
+    the CPU by design (last_hook_path() == HOOK_CPU). The check reads the
+    calling thread's own record, so other threads' calls do not disturb it."""
     r = int(fn(*args))
-    if cpu_fallback_count() != before:
+    if last_hook_path() == HOOK_FALLBACK:
         raise ValError(VAL_ERR_IO, fn.__name__, "GPU path failed: " + last_error())
     return r
 
@@ -400,6 +460,20 @@ def fold_payload_states(state: int, pay_state, pay_len, ok=None) -> tuple[int, i
     r = lib().val_crc32_fold_payload_states(state & 0xFFFFFFFF, ps.ctypes.data, pl.ctypes.data,
                                             okk.ctypes.data if okk is not None else None, ps.size, ctypes.byref(nf))
     return int(r), int(nf.value)
+
+
+def fold_payload_states_at(state: int, pay_state, pay_len, file_off, written: int, ok=None) -> tuple[int, int, int]:
+    """Receiver rolling CRC with its ordering rule -> (state, written, frames folded)."""
+    ps = np.ascontiguousarray(pay_state, dtype=np.uint32)
+    pl = np.ascontiguousarray(pay_len, dtype=np.uint32)
+    fo = np.ascontiguousarray(file_off, dtype=np.uint64)
+    okk = np.ascontiguousarray(ok, dtype=np.uint8) if ok is not None else None
+    w = ctypes.c_uint64(written)
+    nf = ctypes.c_uint32(0)
+    r = lib().val_crc32_fold_payload_states_at(state & 0xFFFFFFFF, ps.ctypes.data, pl.ctypes.data, fo.ctypes.data,
+                                               okk.ctypes.data if okk is not None else None, ps.size,
+                                               ctypes.byref(w), ctypes.byref(nf))
+    return int(r), int(w.value), int(nf.value)
 
 
 def set_host_chunk_bytes(nbytes: int) -> None:

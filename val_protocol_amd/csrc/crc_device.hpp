@@ -26,6 +26,16 @@
 
 #include "gf2_crc32.h"
 
+// Switches that make the kernels return wrong CRCs (A/B diagnostics of the
+// load schedule, the prologue and the region fold) exist only in builds that
+// say so: val_gpu_build_flags() then reports VCRC_DIAG_BUILD, and
+// tests/test_build.py asserts the shipped library reports nothing.
+#if (defined(VCRC_DIAG_NOHASH) || defined(VCRC_NO_LDS_FILL) || defined(VCRC_REGION_HASHONLY) || \
+     defined(VCRC_REGION_NOATOMIC)) &&                                                             \
+    !defined(VCRC_DIAG_BUILD)
+#error "wrong-result diagnostic switches need -DVCRC_DIAG_BUILD (never a product build)"
+#endif
+
 namespace vcrc {
 
 constexpr int kUnit = 64;              // bytes a lane hashes per round

@@ -4,6 +4,7 @@
 // entry point: include/val_crc32_gpu.h.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -11,26 +12,31 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "cpu_crc32.h"
 #include "crc_kernels.hpp"
 #include "val_crc32_gpu.h"
 #include "val_protocol.h"
+#include "val_wire.h"
 
 namespace vcrc {
 
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-// Device scratch of one stream (k_region's accumulator, ragged binning): a
-// stream's calls are ordered by the stream itself, so scratch kept per stream
-// handle needs no events (an event record + wait per call cost ~2.8 us of GPU
-// time on 1 MiB windows, tools/ab_region.py). A destroyed stream's handle is
-// only reused once its work is done, so inheriting its scratch is safe.
-// Callers hold Ctx::mu from acquire through launch.
+// Device scratch of one stream (k_region's accumulator, ragged binning, the
+// dynamic-tail queue): a stream's calls are ordered by the stream itself, so
+// scratch kept per stream needs no events (an event record + wait per call
+// cost ~2.8 us of GPU time on 1 MiB windows, tools/ab_region.py). A stream is
+// keyed by its handle, and hipStreamPerThread (one handle naming a different
+// real stream on every host thread) by handle and thread. A destroyed
+// stream's handle is only reused once its work is done, so inheriting its
+// scratch is safe. Callers hold Ctx::mu from acquire through launch.
 struct Arena {
     uint8_t *d = nullptr;
     size_t cap = 0;
@@ -39,10 +45,14 @@ struct Arena {
 
 struct StreamScratch {
     hipStream_t stream;
+    std::thread::id owner;  // the calling thread for hipStreamPerThread, else none
     Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin;     // ragged binning: counts, plan, sorted order
     Arena queue;   // k_frames dynamic tail {head, exits} (zero between calls)
 };
+// Streams with scratch per device before the list is drained and dropped (a
+// program that keeps creating streams would otherwise grow it without bound).
+constexpr size_t kMaxStreamScratch = 64;
 
 // One context per HIP device: streams, constant blob, staging and scratch.
 // A process may drive any number of devices; each host thread works on the
@@ -154,16 +164,61 @@ val_status_t get_ctx(int device, Ctx **out)
     return VAL_OK;
 }
 
-// The calling thread's context (its bound device, else the process default,
-// else device 0), with the thread's HIP device set to it.
-val_status_t cur(Ctx **out)
+// The caller's HIP device, put back when an entry point returns: the library
+// sets the device it works on (hipSetDevice is per host thread), and must
+// not leave the caller's thread (e.g. torch's) on another one.
+struct DeviceScope {
+    int saved = -1;
+    DeviceScope()
+    {
+        if (hipGetDevice(&saved) != hipSuccess) {
+            (void)hipGetLastError();
+            saved = -1;
+        }
+    }
+    ~DeviceScope()
+    {
+        int now = -1;
+        if (saved >= 0 && hipGetDevice(&now) == hipSuccess && now != saved) (void)hipSetDevice(saved);
+    }
+};
+
+val_status_t ctx_on(int d, Ctx **out)
 {
-    int d = t_dev >= 0 ? t_dev : g_default_dev.load(std::memory_order_relaxed);
-    if (d < 0) d = 0;
     val_status_t st = get_ctx(d, out);
     if (st != VAL_OK) return st;
     VCRC_HIP(hipSetDevice(d), "hipSetDevice");  // device is per host thread in HIP
     return VAL_OK;
+}
+
+// The calling thread's context (its bound device, else the process default,
+// else device 0), with the thread's HIP device set to it. Host-memory calls.
+val_status_t cur(Ctx **out)
+{
+    int d = t_dev >= 0 ? t_dev : g_default_dev.load(std::memory_order_relaxed);
+    if (d < 0) d = 0;
+    return ctx_on(d, out);
+}
+
+// Context of a device-resident call: the device of its stream, else the
+// device `ptr` (the frame or window base) lives on, else the thread's
+// device as in cur(). A cuda:1 tensor on a cuda:1 stream therefore runs on
+// device 1 whatever device the calling thread was bound to.
+val_status_t cur_dev(void *stream, const void *ptr, Ctx **out)
+{
+    const hipStream_t s = (hipStream_t)stream;
+    int d = -1;
+    if (s && s != hipStreamPerThread && s != hipStreamLegacy) {
+        hipDevice_t dev = -1;
+        if (hipStreamGetDevice(s, &dev) == hipSuccess) d = (int)dev;
+        else (void)hipGetLastError();
+    }
+    if (d < 0 && ptr) {
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeDevice) d = attr.device;
+        else (void)hipGetLastError();
+    }
+    return d >= 0 ? ctx_on(d, out) : cur(out);
 }
 
 bool valid_lanes(uint32_t g) { return g == 1 || g == 2 || g == 4 || g == 8 || g == 16 || g == 32 || g == 64; }
@@ -341,9 +396,11 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     const bool one_word = group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_DESC : VCRC_DYN_MIN_GROUP);
     const bool parts =
         group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_PARTS_DESC : VCRC_DYN_MIN_GROUP_PARTS) && group_bytes < VCRC_DYN_MIN_GROUP;
+    // the queue's scratch may be dropped by scratch_for (another stream's call)
+    // unless the lock is held until the kernel is launched
+    Ctx &cm = const_cast<Ctx &>(c);
+    std::lock_guard<std::recursive_mutex> lk(cm.mu);
     if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
-        Ctx &cm = const_cast<Ctx &>(c);
-        std::lock_guard<std::recursive_mutex> lk(cm.mu);
         Arena &a = scratch_for(cm, s).queue;
         uint8_t *q = nullptr;
         val_status_t st = arena_acquire(a, kDynQueueBytes, s, &q);
@@ -415,13 +472,25 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t l
     return launch_uniform_one(c, t, Gt, tl, s);
 }
 
-// Ragged descriptor batch: counting-sort by length on the device, then one
-// grouped launch planned by bytes per length class (no host synchronisation).
+void arena_free(Arena &a);
+
 StreamScratch &scratch_for(Ctx &c, hipStream_t s)
 {
+    const std::thread::id who = s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
     for (StreamScratch *x : c.scratch)
-        if (x->stream == s) return *x;
-    c.scratch.push_back(new StreamScratch{s, {}, {}, {}});
+        if (x->stream == s && x->owner == who) return *x;
+    if (c.scratch.size() >= kMaxStreamScratch) {
+        // every stream drained, so no kernel still uses any of these blocks
+        (void)hipDeviceSynchronize();
+        for (StreamScratch *x : c.scratch) {
+            arena_free(x->region);
+            arena_free(x->queue);
+            arena_free(x->bin);
+            delete x;
+        }
+        c.scratch.clear();
+    }
+    c.scratch.push_back(new StreamScratch{s, who, {}, {}, {}});
     return *c.scratch.back();
 }
 
@@ -450,6 +519,8 @@ void arena_free(Arena &a)
     a = Arena{};
 }
 
+// Ragged descriptor batch: counting-sort by length on the device, then one
+// grouped launch planned by bytes per length class (no host synchronisation).
 val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
 {
     const uint32_t n = p.n;
@@ -620,22 +691,46 @@ bool is_pinned(const void *p)
     return attr.type == hipMemoryTypeHost;
 }
 
-// memcpy with up to 8 host threads (one pinned bounce chunk).
+// memcpy into a pinned bounce chunk with up to 8 host threads, one per 4
+// MiB. Concurrent copies (one per device in the *_host_multi calls) share
+// the process's CPU affinity set: the threads of all copies in flight never
+// exceed it (8 devices x 8 threads would be 64 threads on a 16-core share).
+unsigned host_cpu_budget()
+{
+    static const unsigned n = [] {
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0) return (unsigned)std::max(1, CPU_COUNT(&set));
+        return std::max(1u, std::thread::hardware_concurrency());
+    }();
+    return n;
+}
+
+// Threads one copy of n bytes gets when `concurrent` copies run at once.
+uint32_t copy_threads(uint64_t n, uint32_t concurrent)
+{
+    const uint64_t share = std::max<uint64_t>(1, host_cpu_budget() / std::max<uint32_t>(1, concurrent));
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({8u, share, (n + (4u << 20) - 1) / (4u << 20)}));
+}
+
+std::atomic<uint32_t> g_copies_in_flight{0};
+
 void parallel_copy(uint8_t *dst, const uint8_t *src, size_t n)
 {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nt = std::min<size_t>({8u, hw, (n + (4u << 20) - 1) / (4u << 20)});
+    const uint32_t concurrent = g_copies_in_flight.fetch_add(1) + 1;
+    const size_t nt = copy_threads(n, concurrent);
     if (nt <= 1) {
         memcpy(dst, src, n);
-        return;
+    } else {
+        std::vector<std::thread> th;
+        const size_t per = (n + nt - 1) / nt;
+        for (size_t t = 1; t < nt; t++) {
+            const size_t lo = t * per, hi = std::min(n, lo + per);
+            if (lo < hi) th.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
+        }
+        memcpy(dst, src, std::min(n, per));  // the calling thread takes the first piece
+        for (auto &x : th) x.join();
     }
-    std::vector<std::thread> th;
-    const size_t per = (n + nt - 1) / nt;
-    for (size_t t = 0; t < nt; t++) {
-        const size_t lo = t * per, hi = std::min(n, lo + per);
-        if (lo < hi) th.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
-    }
-    for (auto &x : th) x.join();
+    g_copies_in_flight.fetch_sub(1);
 }
 
 val_status_t grow_pinned(uint8_t **buf, size_t *cap, size_t need)
@@ -674,13 +769,19 @@ val_status_t h2d_staged(Ctx &c, uint8_t *dst, const uint8_t *src, size_t bytes, 
 }
 
 // Wait for a short host-path call (scalar hooks, zero-copy windows): poll
-// hipStreamQuery rather than block in hipStreamSynchronize, about 1 us less
-// per call (provider 16 B: 19.0 -> 17.7 us; profiles/r02_ab_provider_spin.log).
-// The chunked pipeline, whose calls last milliseconds, still blocks.
+// hipStreamQuery for up to kSpinNs, about 1 us less per call than blocking at
+// once (provider 16 B: 19.0 -> 17.7 us; profiles/r02_ab_provider_spin.log),
+// then block in hipStreamSynchronize, so a long call does not burn the core
+// while the caller holds VAL's session mutex. The chunked pipeline, whose
+// calls last milliseconds, blocks from the start.
+constexpr int64_t kSpinNs = 50000;
 hipError_t host_wait(hipStream_t s)
 {
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
     while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+        if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+            return hipStreamSynchronize(s);
     }
     return e;
 }
@@ -689,6 +790,7 @@ hipError_t host_wait(hipStream_t s)
 // hooks and each shard of region_host_multi).
 val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32_t *state_out)
 {
+    DeviceScope ds;
     Ctx *cp = nullptr;
     val_status_t st = cur(&cp);
     if (st != VAL_OK) return st;
@@ -719,18 +821,42 @@ val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32
     return VAL_OK;
 }
 
-// ---- failure policy of the scalar hooks ---------------------------------------
+// ---- the scalar hooks: CPU below a size threshold, GPU above -----------------
 // crc32_func_t has no error channel (reference include/val_protocol.h:163-166)
 // and the reference calls it under the session mutex on every frame
-// (src/val_core.c:721-836, :884-1045): it must return the right CRC. When the
-// GPU path fails (no device, a HIP error), the three scalar hooks compute the
-// CRC with this library's own CPU slice-by-8 (cpu_update below) and count it
-// (val_gpu_cpu_fallback_count); nothing else has a CPU path, and the batch
-// calls return VAL_ERR_IO. VAL_GPU_CPU_FALLBACK=0 or
-// val_gpu_set_cpu_fallback(0) makes a failed hook abort instead. The GPU test
-// suite asserts the count stays 0, so no result it checks came from here.
+// (src/val_core.c:721-836, :884-1045) with host memory in and one CRC out.
+// A GPU call costs a launch and a completion wait (~18 us) plus the bytes
+// over PCIe, while the reference's byte loop costs ~1.7 us per KiB: below the
+// provider threshold the three scalar hooks answer with this library's own
+// CPU engine (cpu_crc32.c: carry-less-multiply folding, slice-by-16 where the
+// CPU lacks it), so installing the provider never makes VAL slower. At and
+// above the threshold they run on the GPU. The threshold is measured
+// (tools/provider_latency.py); VAL_GPU_PROVIDER_MIN_BYTES
+// or val_gpu_set_provider_min_bytes overrides it (0 = always the GPU: the GPU
+// test suite sets it, so every hook it checks ran on the GPU).
+// Failure policy: when the GPU path fails (no device, a HIP error), the hooks
+// compute the CRC with the same CPU engine and count it
+// (val_gpu_cpu_fallback_count); VAL_GPU_CPU_FALLBACK=0 or
+// val_gpu_set_cpu_fallback(0) makes a failed hook abort instead. Nothing else
+// has a CPU path: batch calls return VAL_ERR_IO.
 std::atomic<uint64_t> g_cpu_fallbacks{0};
+std::atomic<uint64_t> g_cpu_small{0};
 std::atomic<int> g_cpu_fallback_on{-1};  // -1: from the environment
+std::atomic<int64_t> g_provider_min{-1};  // -1: from the environment, else the default
+thread_local int t_hook_path = VAL_GPU_HOOK_NONE;
+
+#ifndef VCRC_PROVIDER_MIN_BYTES  // measured crossover, DESIGN.md section 1
+#define VCRC_PROVIDER_MIN_BYTES (1u << 20)
+#endif
+
+uint64_t provider_min_bytes()
+{
+    const int64_t v = g_provider_min.load(std::memory_order_relaxed);
+    if (v >= 0) return (uint64_t)v;
+    static const int64_t env = getenv("VAL_GPU_PROVIDER_MIN_BYTES") ? strtoll(getenv("VAL_GPU_PROVIDER_MIN_BYTES"), nullptr, 0)
+                                                                    : -1;
+    return env >= 0 ? (uint64_t)env : (uint64_t)VCRC_PROVIDER_MIN_BYTES;
+}
 
 bool cpu_fallback_enabled()
 {
@@ -738,37 +864,6 @@ bool cpu_fallback_enabled()
     if (v >= 0) return v != 0;
     const char *e = getenv("VAL_GPU_CPU_FALLBACK");
     return !(e && e[0] == '0');
-}
-
-// Slice-by-8 tables S_k[b] = b * x^(8(k+1)) mod P (S_0 = the reference's
-// table, src/val_core.c:133-148), built from the GF(2) helpers once.
-struct CpuTables {
-    uint32_t t[8][256];
-    CpuTables()
-    {
-        for (int k = 0; k < 8; k++) {
-            const uint32_t xk = gf2_x8n((uint64_t)(k + 1));
-            for (int b = 0; b < 256; b++) t[k][b] = gf2_mul(xk, (uint32_t)b);
-        }
-    }
-};
-
-uint32_t cpu_update(uint32_t c, const void *data, size_t len)
-{
-    static const CpuTables T;
-    const uint8_t *p = static_cast<const uint8_t *>(data);
-    while (len >= 8) {
-        uint32_t lo, hi;
-        memcpy(&lo, p, 4);
-        memcpy(&hi, p + 4, 4);
-        lo ^= c;
-        c = T.t[7][lo & 0xFF] ^ T.t[6][(lo >> 8) & 0xFF] ^ T.t[5][(lo >> 16) & 0xFF] ^ T.t[4][lo >> 24] ^
-            T.t[3][hi & 0xFF] ^ T.t[2][(hi >> 8) & 0xFF] ^ T.t[1][(hi >> 16) & 0xFF] ^ T.t[0][hi >> 24];
-        p += 8;
-        len -= 8;
-    }
-    while (len--) c = T.t[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
-    return c;
 }
 
 [[noreturn]] void die(const char *fn)
@@ -781,12 +876,21 @@ uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t l
 {
     uint32_t out = 0;
     if (len && !data) die(fn);  // the reference dereferences it too
-    if (region_host(data, len, state, &out) == VAL_OK) return out;
+    if ((uint64_t)len < provider_min_bytes()) {
+        t_hook_path = VAL_GPU_HOOK_CPU;
+        g_cpu_small.fetch_add(1, std::memory_order_relaxed);
+        return vcrc_cpu_update(state, data, len);
+    }
+    if (region_host(data, len, state, &out) == VAL_OK) {
+        t_hook_path = VAL_GPU_HOOK_GPU;
+        return out;
+    }
     if (!cpu_fallback_enabled()) die(fn);
+    t_hook_path = VAL_GPU_HOOK_FALLBACK;
     if (g_cpu_fallbacks.fetch_add(1, std::memory_order_relaxed) == 0)
         fprintf(stderr, "val_crc32_gpu: %s: GPU path failed (%s); CRC computed on the CPU (counted)\n", fn,
                 t_err.c_str());
-    return cpu_update(state, data, len);
+    return vcrc_cpu_update(state, data, len);
 }
 
 // Small host windows (<= 256 KiB of wire span): one launch and no copy
@@ -882,6 +986,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         lmax = std::max<uint32_t>(lmax, (uint32_t)l);
         if (off && i && off[i] < off[i - 1]) monotone = false;
     }
+    DeviceScope ds;
     Ctx *cp = nullptr;
     val_status_t st = cur(&cp);
     if (st != VAL_OK) return st;
@@ -1164,6 +1269,34 @@ uint32_t fold_payloads(uint32_t state, const uint32_t *pay_state, const uint32_t
     return state;
 }
 
+// The same fold with the receiver's ordering rule (reference
+// src/val_receiver.c:871-891, offsets from src/val_core.c:981-993): a DATA
+// frame whose effective offset (its explicit offset, or *written when the
+// offset is implied) equals *written is folded and advances *written by its
+// payload; an earlier offset is a duplicate and a later one a gap: neither
+// is folded, and later frames are still judged one by one, as the receiver
+// does. Frames with ok[i] == 0 (trailer mismatch) and non-DATA frames
+// (VAL_FRAME_OFFSET_NOT_DATA) are never folded.
+uint32_t fold_payloads_at(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len, const uint64_t *file_off,
+                          const uint8_t *ok, uint32_t n, uint64_t *written, uint32_t *n_folded)
+{
+    ShiftMap m;
+    uint64_t w = *written;
+    uint32_t folded = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((ok && !ok[i]) || file_off[i] == VAL_FRAME_OFFSET_NOT_DATA) continue;
+        const uint64_t eff = file_off[i] == VAL_FRAME_OFFSET_IMPLIED ? w : file_off[i];
+        if (eff != w) continue;
+        m.set(pay_len[i]);
+        state = m.apply(state) ^ pay_state[i];
+        w += pay_len[i];
+        folded++;
+    }
+    *written = w;
+    if (n_folded) *n_folded = folded;
+    return state;
+}
+
 void ctx_free(Ctx &c)
 {
     if (c.device >= 0) (void)hipSetDevice(c.device);
@@ -1281,6 +1414,59 @@ int vcrc_debug_info(uint32_t *out)
 
 const char *val_gpu_last_error(void) { return t_err.c_str(); }
 
+const char *val_gpu_build_flags(void)
+{
+    // every compile-time switch of the sources, diagnostic or A/B, that is set
+    static const char flags[] = ""
+#ifdef VCRC_DIAG_BUILD
+                                " VCRC_DIAG_BUILD"
+#endif
+#ifdef VCRC_DIAG_NOHASH
+                                " VCRC_DIAG_NOHASH"
+#endif
+#ifdef VCRC_NO_LDS_FILL
+                                " VCRC_NO_LDS_FILL"
+#endif
+#ifdef VCRC_REGION_HASHONLY
+                                " VCRC_REGION_HASHONLY"
+#endif
+#ifdef VCRC_REGION_NOATOMIC
+                                " VCRC_REGION_NOATOMIC"
+#endif
+#ifdef VCRC_TIMING
+                                " VCRC_TIMING"
+#endif
+#ifdef VCRC_NO_SPLIT
+                                " VCRC_NO_SPLIT"
+#endif
+#ifdef VCRC_NO_KARG_EARLY
+                                " VCRC_NO_KARG_EARLY"
+#endif
+        ;
+    return flags[0] ? flags + 1 : flags;
+}
+
+void val_gpu_set_provider_min_bytes(int64_t bytes) { g_provider_min.store(bytes < 0 ? -1 : bytes); }
+
+uint64_t val_gpu_provider_min_bytes(void) { return provider_min_bytes(); }
+
+uint64_t val_gpu_cpu_small_count(void) { return g_cpu_small.load(std::memory_order_relaxed); }
+
+int val_gpu_last_hook_path(void) { return t_hook_path; }
+
+uint32_t val_crc32_cpu_update_state(uint32_t state, const void *data, size_t len, int engine)
+{
+    if (len && !data) return state;
+    return vcrc_cpu_update_with(engine, state, data, len);
+}
+
+int val_crc32_cpu_engine(void) { return vcrc_cpu_engine(); }
+
+uint32_t val_gpu_host_copy_threads(uint64_t bytes, uint32_t concurrent_copies)
+{
+    return copy_threads(bytes, concurrent_copies);
+}
+
 uint64_t val_gpu_cpu_fallback_count(void) { return g_cpu_fallbacks.load(std::memory_order_relaxed); }
 
 void val_gpu_set_cpu_fallback(int enable) { g_cpu_fallback_on.store(enable < 0 ? -1 : (enable ? 1 : 0)); }
@@ -1302,6 +1488,7 @@ val_status_t val_gpu_set_host_chunk_bytes(size_t bytes)
 
 void *val_gpu_host_alloc(size_t bytes)
 {
+    DeviceScope ds;
     Ctx *c = nullptr;
     if (cur(&c) != VAL_OK) return nullptr;
     void *p = nullptr;
@@ -1375,8 +1562,9 @@ val_status_t val_crc32_frames_dev(const uint8_t *d_base, const uint64_t *d_off, 
     t_err.clear();
     if ((d_off == nullptr) != (d_len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
     if (!d_base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
+    DeviceScope ds;
     Ctx *c = nullptr;
-    val_status_t st = cur(&c);
+    val_status_t st = cur_dev(stream, d_base, &c);
     if (st != VAL_OK) return st;
     FrameParams p{};
     p.base = d_base;
@@ -1400,8 +1588,9 @@ val_status_t val_crc32_verify_frames_dev(const uint8_t *d_base, const uint64_t *
     t_err.clear();
     if ((d_off == nullptr) != (d_len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
     if (!d_base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
+    DeviceScope ds;
     Ctx *c = nullptr;
-    val_status_t st = cur(&c);
+    val_status_t st = cur_dev(stream, d_base, &c);
     if (st != VAL_OK) return st;
     FrameParams p{};
     p.base = d_base;
@@ -1426,8 +1615,9 @@ val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t s
 {
     t_err.clear();
     if (!d_state_out || (!d_ptr && len)) return fail(VAL_ERR_INVALID_ARG, "NULL pointer");
+    DeviceScope ds;
     Ctx *c = nullptr;
-    val_status_t st = cur(&c);
+    val_status_t st = cur_dev(stream, d_ptr, &c);
     if (st != VAL_OK) return st;
     return region_dev(*c, d_ptr, len, state_in, d_state_out, pick_stream(stream));
 }
@@ -1481,8 +1671,9 @@ val_status_t val_crc32_verify_frames_ex_dev(const uint8_t *d_base, const uint64_
     t_err.clear();
     if ((d_off == nullptr) != (d_len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
     if (!d_base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
+    DeviceScope ds;
     Ctx *c = nullptr;
-    val_status_t st = cur(&c);
+    val_status_t st = cur_dev(stream, d_base, &c);
     if (st != VAL_OK) return st;
     FrameParams p{};
     p.base = d_base;
@@ -1523,6 +1714,17 @@ uint32_t val_crc32_fold_payload_states(uint32_t state, const uint32_t *pay_state
         return state;
     }
     return fold_payloads(state, pay_state, pay_len, ok, n, n_folded);
+}
+
+uint32_t val_crc32_fold_payload_states_at(uint32_t state, const uint32_t *pay_state, const uint32_t *pay_len,
+                                          const uint64_t *file_off, const uint8_t *ok, uint32_t n, uint64_t *written,
+                                          uint32_t *n_folded)
+{
+    if (!pay_state || !pay_len || !file_off || !written) {
+        if (n_folded) *n_folded = 0;
+        return state;
+    }
+    return fold_payloads_at(state, pay_state, pay_len, file_off, ok, n, written, n_folded);
 }
 
 val_status_t val_crc32_region_host_multi(const void *data, uint64_t len, uint32_t state_in, uint32_t *state_out,

@@ -88,4 +88,22 @@ def payload_lens(stream: np.ndarray, frame_off, crc_len) -> np.ndarray:
     return out
 
 
-__all__ = ["serialize_header", "deserialize_header", "build_data_batch", "put_trailers", "scan_frames", "payload_lens", "ValError"]
+# val_frame_data_offsets sentinels (val_wire.h)
+OFFSET_IMPLIED = (1 << 64) - 1
+OFFSET_NOT_DATA = (1 << 64) - 2
+
+
+def data_offsets(stream: np.ndarray, frame_off, crc_len) -> np.ndarray:
+    """File offset of each frame as the receiver reads it (val_frame_data_offsets):
+    explicit offset, OFFSET_IMPLIED or OFFSET_NOT_DATA."""
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    frame_off = np.ascontiguousarray(frame_off, dtype=np.uint64)
+    crc_len = np.ascontiguousarray(crc_len, dtype=np.uint32)
+    out = np.zeros(crc_len.size, dtype=np.uint64)
+    lib().val_frame_data_offsets(stream.ctypes.data, frame_off.ctypes.data, crc_len.ctypes.data, crc_len.size,
+                                 out.ctypes.data)
+    return out
+
+
+__all__ = ["serialize_header", "deserialize_header", "build_data_batch", "put_trailers", "scan_frames", "payload_lens",
+           "data_offsets", "OFFSET_IMPLIED", "OFFSET_NOT_DATA", "ValError"]
