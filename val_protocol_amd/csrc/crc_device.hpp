@@ -72,14 +72,16 @@ __device__ __forceinline__ uint32_t lds_read(uint32_t byte_addr)
 __device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const u32u *>(p); }
 __device__ __forceinline__ uint32_t ld32(gu8 *p) { return *reinterpret_cast<gu32u *>(p); }
 
-// Per-lane LDS bases of the slice tables (T3 consumes the first byte of a word).
+// Per-lane LDS bases of the slice tables (T3 consumes the first byte of a
+// word): the pair bases T3 and T1; T2 and T0 sit 128 B above them (the half),
+// reached through the ds_read offset field, so two VGPRs hold all four.
 struct SliceBases {
-    uint32_t t3, t2, t1, t0;
+    uint32_t t3, t1;
 };
 
 __device__ __forceinline__ SliceBases slice_bases(uint32_t lo4)
 {
-    return SliceBases{kLdsS4 + lo4, kLdsS4 + 128u + lo4, kLdsS4 + 65536u + lo4, kLdsS4 + 65536u + 128u + lo4};
+    return SliceBases{kLdsS4 + lo4, kLdsS4 + 65536u + lo4};
 }
 
 // v_perm_b32 builds [base.b0 | y.byte_k | base.b2 | 0] = the table address.
@@ -93,16 +95,16 @@ __device__ __forceinline__ uint32_t s4_step(uint32_t c, uint32_t w, const SliceB
 {
     const uint32_t y = c ^ w;
 #ifdef VCRC_DIAG_NOHASH  // diagnostic A/B builds only (wrong CRCs): the load schedule without the table work
-    return y + b.t0;
+    return y + b.t1;
 #endif
-    return lds_read(tab_addr(y, b.t3, 0)) ^ lds_read(tab_addr(y, b.t2, 1)) ^ lds_read(tab_addr(y, b.t1, 2)) ^
-           lds_read(tab_addr(y, b.t0, 3));
+    return lds_read(tab_addr(y, b.t3, 0)) ^ lds_read(tab_addr(y, b.t3, 1) + 128u) ^ lds_read(tab_addr(y, b.t1, 2)) ^
+           lds_read(tab_addr(y, b.t1, 3) + 128u);
 }
 
 // Classic byte step c = T0[(c ^ byte) & 0xff] ^ (c >> 8) (reference val_core.c:157).
 __device__ __forceinline__ uint32_t byte_step(uint32_t c, uint32_t byte, const SliceBases &b)
 {
-    return lds_read(tab_addr(c ^ byte, b.t0, 0)) ^ (c >> 8);
+    return lds_read(tab_addr(c ^ byte, b.t1, 0) + 128u) ^ (c >> 8);
 }
 
 // Advance register a by the distance of the nibble map at byte address

@@ -846,7 +846,7 @@ std::atomic<int64_t> g_provider_min{-1};  // -1: from the environment, else the 
 thread_local int t_hook_path = VAL_GPU_HOOK_NONE;
 
 #ifndef VCRC_PROVIDER_MIN_BYTES  // measured crossover, DESIGN.md section 1
-#define VCRC_PROVIDER_MIN_BYTES (1u << 20)
+#define VCRC_PROVIDER_MIN_BYTES (256u << 20)
 #endif
 
 uint64_t provider_min_bytes()
