@@ -288,12 +288,30 @@ int prefetch_depth()
     return forced >= 0 ? forced : 1;
 }
 
+// Carried frames (k_frames_carry: the next group's first loads issued during
+// this group's last round) at G <= 4 and the default depth, payload states
+// excepted: VAL_GPU_CARRY=0 (or -DVCRC_CARRY_DEFAULT=0) selects k_frames<G, 1>.
+#ifndef VCRC_CARRY_DEFAULT
+#define VCRC_CARRY_DEFAULT 1
+#endif
+bool carry_enabled()
+{
+    static const bool on = getenv("VAL_GPU_CARRY") ? atoi(getenv("VAL_GPU_CARRY")) != 0 : VCRC_CARRY_DEFAULT != 0;
+    return on;
+}
+
 template <int G>
 void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
 {
     if (p.out_pay) {  // payload states: the default depth only
         hipLaunchKernelGGL((k_frames<G, 1, true>), grid, dim3(kBlock), 0, s, p);
         return;
+    }
+    if constexpr (G >= 2 && G <= 4) {
+        if (pf == 1 && carry_enabled()) {
+            hipLaunchKernelGGL((k_frames_carry<G>), grid, dim3(kBlock), 0, s, p);
+            return;
+        }
     }
     switch (pf) {
     case 0: hipLaunchKernelGGL((k_frames<G, 0, false>), grid, dim3(kBlock), 0, s, p); break;
@@ -1083,6 +1101,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         VCRC_HIP(hipStreamWaitEvent(s, c.h2d_done[k], 0), "hipStreamWaitEvent");
         FrameParams p{};
         p.base = c.d_slot[k] - ch.lo;  // the kernel only touches base + off within the slot
+        p.lo_off = off ? ch.lo : 0u;
         p.off = d_off ? d_off + ch.i0 : nullptr;
         p.len = d_len ? d_len + ch.i0 : nullptr;
         if (!off) p.base = c.d_slot[k];  // strided: frame i0 is at the slot start
