@@ -471,6 +471,10 @@ def main():
                 # same box, same buffer: plain read-only stream (bench/roof.hip); SURVEY 8(d)
                 "read_roof": round(roof, 1) if roof else None,
                 "frac_of_read_roof": round(achieved_gbs / roof, 4) if roof else None,
+                # the plain-load roof itself as a share of the spec peak: when it is
+                # below 0.80, the 80% target sits above what any read of this buffer
+                # reaches on this box
+                "read_roof_frac_of_peak": round(roof / HBM_PEAK_GBS, 4) if roof else None,
             },
             "cpu_baseline": cpu,
             # per-GPU rates and the aggregate's denominator (BASELINE configs[3])
