@@ -78,7 +78,6 @@ struct FrameParams {
     uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
     uint32_t qparts;         // with qhead: queue partitions, 1..kDynParts
     uint32_t r0x4;           // uniform batches: whole round-0 units by dwordx4 (load_unit0)
-    uint64_t lo_off;         // base + lo_off is the first byte the batch's buffer holds (k_frames_carry)
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -230,9 +229,14 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 // PAY: also write the payload state (p.out_pay); a separate instantiation so
 // the TX and plain verify kernels carry none of its registers.
 // BF: branch-free round-0 loads (load_unit0); k_region only.
-template <int GT, int PF, bool PAY, bool BF, typename Pre>
+// mid() runs once round 0 is hashed (all 64 lanes, wave-uniform): the ragged
+// kernel fetches its next item's descriptors there.
+struct NoMid {
+    __device__ void operator()() const {}
+};
+template <int GT, int PF, bool PAY, bool BF, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           const SliceBases &sb, int Gr, Pre &&pre)
+                                           const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
     constexpr int D = PF > 0 ? PF : 1;
     const int G = GT ? GT : Gr;
@@ -302,6 +306,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
             for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
         }
     }
+    mid();
     // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, round 1).
     const bool seed_spill = g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1;
     if (PF == 0) {
@@ -425,33 +430,55 @@ __device__ __forceinline__ Geo frame_geo(const uint8_t *base, uint64_t off, uint
     return q;
 }
 
-// A frame's rounds 0 (w0) and 1 (nxt, when it has one). Unit 0 is read whole
-// (its bytes before the frame are masked later): sixteen clamped dword loads
-// need sixteen addresses live at once, which spilled in the last round. A
-// unit 0 that would start before the batch's buffer (off < lo_off + pad: the
-// buffer's first frame) is left to unit0_near_base when the frame's hashing
-// starts.
-__device__ __forceinline__ bool unit0_near_base(const Geo &q, uint64_t off, uint64_t lo_off)
+// Unit 0 through its frame's first line. Unit 0 starts pad bytes before the
+// frame, so read whole it can reach into the previous 128-B line (the previous
+// frame's end, which that frame reads a group-time later: 1,100-B frames read
+// 1.30x their bytes that way, against 1.12x with clamped loads). Sixteen
+// clamped dword loads need sixteen live addresses, which spilled in the last
+// round. Here the 64 B are read from A = max(unit start, the frame's first
+// line) by four dwordx4 loads, never outside that line (A is dword-aligned and
+// A + 64 stays in the line), and moved up by the s = (A - unit start) / 4
+// words skipped: a four-stage select network. The words before the frame are
+// masked later (unit0_finish). A line never crosses a page, so the read is
+// safe even for a frame at the very start of its buffer.
+// (The loads are issued by load_unit0_line, the words moved by
+// unit0_line_shift where they are used: the shift amount is recomputed, so
+// nothing extra stays live in between.)
+__device__ __forceinline__ uint32_t unit0_line_skip(gu8 *fp, uint32_t pad)  // bytes of unit 0 before fp's line
 {
-    return q.u0 == 0 && q.Lg >= 4 && off < lo_off + q.pad;
+    const uint32_t in_line = (uint32_t)((uintptr_t)fp & 127u);
+    return pad > in_line ? pad - in_line : 0u;
 }
-__device__ __forceinline__ void load_r01(uint32_t (&w0)[kWords], uint32_t (&nxt)[kWords], const Geo &q, uint64_t off,
-                                         uint64_t lo_off, int G)
+__device__ __forceinline__ void load_unit0_line(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
 {
-    if (q.u0 >= 0 && q.Lg >= 4 && !unit0_near_base(q, off, lo_off)) load_full(w0, q.fp + (int64_t)q.u0 * kUnit - q.pad);
+    load_full(w, fp - pad + unit0_line_skip(fp, pad));
+}
+__device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
+{
+    const uint32_t sh = unit0_line_skip(fp, pad) >> 2;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int d = 1 << b;
+        const bool on = (sh >> b) & 1u;
+#pragma unroll
+        for (int i = kWords - 1; i >= 0; i--) w[i] = on ? (i >= d ? w[i - d] : 0u) : w[i];
+    }
+}
+
+// A frame's rounds 0 (w0) and 1 (nxt, when it has one).
+__device__ __forceinline__ void load_r01(uint32_t (&w0)[kWords], uint32_t (&nxt)[kWords], const Geo &q, int G)
+{
+    if (q.u0 > 0 && q.Lg >= 4) load_full(w0, q.fp + (int64_t)q.u0 * kUnit - q.pad);
+    if (q.u0 == 0 && q.Lg >= 4) load_unit0_line(w0, q.fp, q.pad);
     if (q.R >= 2u) load_full(nxt, q.fp + ((int64_t)q.u0 + G) * kUnit - q.pad);
 }
 
 template <int G, typename Next>
-__device__ __forceinline__ void hash_frame_carry(const FrameParams &p, uint32_t f, bool active, const Geo &q, uint64_t off,
+__device__ __forceinline__ void hash_frame_carry(const FrameParams &p, uint32_t f, bool active, const Geo &q,
                                                  uint32_t (&w0)[kWords], uint32_t (&nxt)[kWords], int g,
                                                  const SliceBases &sb, Next &&next)
 {
     constexpr int lgG = ilog2(G);
-    if (unit0_near_base(q, off, p.lo_off)) {  // clamped loads, never before the frame's first dword
-        gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
-        load_unit0<false>(w0, 0, q.fp, q.Lg, q.pad, dummy, false);
-    }
     const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
     const bool hdr = q.R > 0 && q.u0 == 0 && p.out_hdr;
     const bool last_lane = active && g == G - 1;
@@ -480,6 +507,7 @@ __device__ __forceinline__ void hash_frame_carry(const FrameParams &p, uint32_t 
     uint32_t w[kWords];
 #pragma unroll
     for (int i = 0; i < kWords; i++) w[i] = w0[i];
+    if (q.u0 == 0 && q.Lg >= 4) unit0_line_shift(w, q.fp, q.pad);
     if (q.R <= 1u) {  // round 0 is the last round
         issue_end();
         next(w0, nxt);
@@ -724,7 +752,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_carry(const FrameParams p)
     bool acta = ga + (uint64_t)slot < p.n;
     if (acta) frame_desc(p, fa, offa, La);
     uint32_t w0[kWords], nxt[kWords];
-    load_r01(w0, nxt, frame_geo(p.base, offa, La, acta, g, G, lgG), offa, p.lo_off, G);
+    load_r01(w0, nxt, frame_geo(p.base, offa, La, acta, g, G, lgG), G);
     // the LDS fill and the barrier run under the first frame's memory latency
     lds_tables_write(im);
     __syncthreads();
@@ -742,9 +770,9 @@ __global__ __launch_bounds__(kBlock) void k_frames_carry(const FrameParams p)
             bool deq_c;
             const uint64_t gc = succ(gb, deq_c);
             const uint32_t kc = deq_c ? dequeue() : 0u;
-            hash_frame_carry<G>(p, fa, acta, frame_geo(p.base, offa, La, acta, g, G, lgG), offa, w0, nxt, g, sb,
+            hash_frame_carry<G>(p, fa, acta, frame_geo(p.base, offa, La, acta, g, G, lgG), w0, nxt, g, sb,
                                 [&](uint32_t(&a)[kWords], uint32_t(&b)[kWords]) {
-                                    load_r01(a, b, frame_geo(p.base, offb, Lb, actb, g, G, lgG), offb, p.lo_off, G);
+                                    load_r01(a, b, frame_geo(p.base, offb, Lb, actb, g, G, lgG), G);
                                 });
             if (gb == kNone) break;
             fa = fb;
@@ -996,34 +1024,38 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     const uint32_t k0 = (blockIdx.x / P) * kWavesPerBlock + (threadIdx.x >> 6);
     uint32_t it = part + P * k0;
     if (it >= items) return;
-    uint32_t it_n = part + P * (k0 + nwp);  // second item: static
     Item cur = ragged_item(ctab, it);
     uint64_t f, off;
     uint32_t L;
     bool active;
     item_frame(p, cur, lane, f, active, off, L, ident);
+    // One item ahead: the next item is dequeued when this one starts, and its
+    // descriptors are fetched once this one's round 0 is hashed (the atomic
+    // has long returned). When the queue runs dry each wave has one item left
+    // to hash, not two (a two-ahead queue left up to two items per wave).
     while (true) {
-        // dequeue item i + 2 (its index is only needed next iteration)
-        uint32_t k_nn = 0;
-        if (it_n < items && lane == 0) k_nn = atomicAdd(head, 1u);
-        Item nxt{0, 0, 0};
+        uint32_t k_n = 0;
+        if (lane == 0) k_n = atomicAdd(head, 1u);
+        Item nx{0, 0, 0};
+        uint32_t it_n = items;
         uint64_t f_n = 0, off_n = 0;
         uint32_t L_n = 0;
         bool active_n = false;
-        if (it_n < items) {
-            nxt = ragged_item(ctab, it_n);
-            item_frame(p, nxt, lane, f_n, active_n, off_n, L_n, ident);
-        }
         const int G = class_lanes(cur.c);
         VCRC_LAST_ITEM(cur.c, L);
-        hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {});
+        hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {}, [&] {
+            it_n = part + P * (__builtin_amdgcn_readfirstlane(k_n) + nwp);
+            if (it_n < items) {
+                nx = ragged_item(ctab, it_n);
+                item_frame(p, nx, lane, f_n, active_n, off_n, L_n, ident);
+            }
+        });
         if (it_n >= items) {
             VCRC_STAMP(2);
             break;
         }
         it = it_n;
-        it_n = part + P * (__builtin_amdgcn_readfirstlane(k_nn) + 2u * nwp);
-        cur = nxt;
+        cur = nx;
         f = f_n;
         off = off_n;
         L = L_n;

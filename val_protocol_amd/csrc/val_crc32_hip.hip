@@ -1101,7 +1101,6 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         VCRC_HIP(hipStreamWaitEvent(s, c.h2d_done[k], 0), "hipStreamWaitEvent");
         FrameParams p{};
         p.base = c.d_slot[k] - ch.lo;  // the kernel only touches base + off within the slot
-        p.lo_off = off ? ch.lo : 0u;
         p.off = d_off ? d_off + ch.i0 : nullptr;
         p.len = d_len ? d_len + ch.i0 : nullptr;
         if (!off) p.base = c.d_slot[k];  // strided: frame i0 is at the slot start
