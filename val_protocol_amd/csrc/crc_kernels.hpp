@@ -101,6 +101,41 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
     }
 }
 
+// Unit 0 through its frame's first line. Unit 0 starts pad bytes before the
+// frame, so read whole it can reach into the previous 128-B line (the previous
+// frame's end, which that frame reads a group-time later: 1,100-B frames read
+// 1.30x their bytes that way, against 1.12x with clamped loads). Sixteen
+// clamped dword loads need sixteen live addresses, which spilled in the last
+// round. Here the 64 B are read from A = max(unit start, the frame's first
+// line) by four dwordx4 loads, never outside that line (A is dword-aligned and
+// A + 64 stays in the line), and moved up by the s = (A - unit start) / 4
+// words skipped: a four-stage select network. The words before the frame are
+// masked later (unit0_finish). A line never crosses a page, so the read is
+// safe even for a frame at the very start of its buffer.
+// (The loads are issued by load_unit0_line, the words moved by
+// unit0_line_shift where they are used: the shift amount is recomputed, so
+// nothing extra stays live in between.)
+__device__ __forceinline__ uint32_t unit0_line_skip(gu8 *fp, uint32_t pad)  // bytes of unit 0 before fp's line
+{
+    const uint32_t in_line = (uint32_t)((uintptr_t)fp & 127u);
+    return pad > in_line ? pad - in_line : 0u;
+}
+__device__ __forceinline__ void load_unit0_line(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
+{
+    load_full(w, fp - pad + unit0_line_skip(fp, pad));
+}
+__device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
+{
+    const uint32_t sh = unit0_line_skip(fp, pad) >> 2;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int d = 1 << b;
+        const bool on = (sh >> b) & 1u;
+#pragma unroll
+        for (int i = kWords - 1; i >= 0; i--) w[i] = on ? (i >= d ? w[i - d] : 0u) : w[i];
+    }
+}
+
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
 // first unit, with the seed in frame bytes 0..3; u < 0 nothing. Lg = bytes on
 // the unit grid; Lg < 4 frames take the byte path (tiny). Loads only, into
@@ -132,6 +167,10 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp
                                            bool r0x4)
 {
     const bool has = u >= 0 && Lg >= 4;
+    if (!BF && has && u == 0) {  // k_frames, ragged: four dwordx4 loads inside the frame's first line
+        load_unit0_line(w, fp, pad);
+        return;
+    }
     if (BF || has) {
         gu8 *base = has ? fp + ((int64_t)u * kUnit - pad) : dummy;
         const uint32_t lo = (has && u == 0) ? (pad & ~3u) : 0u;
@@ -299,6 +338,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
+        if (!BF && u0 == 0 && Lg >= 4) unit0_line_shift(w0, fp, pad);
         unit0_finish(w0, u0, Lg, pad, seed);
         acc = s4_words_from(first, w0, sb);
         if (tiny) {  // Lg < 4: state of all L bytes straight from the seed
@@ -428,41 +468,6 @@ __device__ __forceinline__ Geo frame_geo(const uint8_t *base, uint64_t off, uint
     q.pad = q.U * kUnit - q.Lg;
     q.u0 = (int)q.U - G * (int)q.R + g;
     return q;
-}
-
-// Unit 0 through its frame's first line. Unit 0 starts pad bytes before the
-// frame, so read whole it can reach into the previous 128-B line (the previous
-// frame's end, which that frame reads a group-time later: 1,100-B frames read
-// 1.30x their bytes that way, against 1.12x with clamped loads). Sixteen
-// clamped dword loads need sixteen live addresses, which spilled in the last
-// round. Here the 64 B are read from A = max(unit start, the frame's first
-// line) by four dwordx4 loads, never outside that line (A is dword-aligned and
-// A + 64 stays in the line), and moved up by the s = (A - unit start) / 4
-// words skipped: a four-stage select network. The words before the frame are
-// masked later (unit0_finish). A line never crosses a page, so the read is
-// safe even for a frame at the very start of its buffer.
-// (The loads are issued by load_unit0_line, the words moved by
-// unit0_line_shift where they are used: the shift amount is recomputed, so
-// nothing extra stays live in between.)
-__device__ __forceinline__ uint32_t unit0_line_skip(gu8 *fp, uint32_t pad)  // bytes of unit 0 before fp's line
-{
-    const uint32_t in_line = (uint32_t)((uintptr_t)fp & 127u);
-    return pad > in_line ? pad - in_line : 0u;
-}
-__device__ __forceinline__ void load_unit0_line(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
-{
-    load_full(w, fp - pad + unit0_line_skip(fp, pad));
-}
-__device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
-{
-    const uint32_t sh = unit0_line_skip(fp, pad) >> 2;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const int d = 1 << b;
-        const bool on = (sh >> b) & 1u;
-#pragma unroll
-        for (int i = kWords - 1; i >= 0; i--) w[i] = on ? (i >= d ? w[i - d] : 0u) : w[i];
-    }
 }
 
 // A frame's rounds 0 (w0) and 1 (nxt, when it has one).
