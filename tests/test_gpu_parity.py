@@ -543,8 +543,9 @@ def test_wave_round_tail(vc, dev, L, extra):
 @pytest.mark.parametrize("strided,payload,per", [
     (True, 16384, 8),    # strided groups of 8 x 16 KiB: one queue word
     (False, 65516, 4),   # descriptor groups of 4 x 64 KiB: one queue word
-    (True, 4184, 16),    # strided groups of 16 x 4.2 KiB (67 KB): 64 queue partitions
-    (False, 4184, 16),   # descriptor groups of 16 x 4.2 KiB: 64 queue partitions
+    (True, 4184, 8),     # strided groups of 8 x 4.2 KiB (34 KB): 64 queue partitions
+    (False, 4184, 8),    # descriptor groups of 8 x 4.2 KiB: 64 queue partitions
+    (False, 1084, 16),   # descriptor groups of 16 x 1.1 KiB (k_frames_carry): 64 queue partitions
 ])
 def test_dynamic_tail_every_frame(vc, dev, strided, payload, per):
     """Launches long enough for the dynamic tail (k_frames: the last half of

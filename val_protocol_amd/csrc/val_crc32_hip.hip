@@ -241,11 +241,17 @@ uint32_t forced_lanes()
     return valid_lanes(env_g) ? env_g : 0u;
 }
 
-// Lanes that share one frame (G): the length class's measured best.
+// Lanes that share one frame (G) in uniform batches, by length: the measured
+// best of the current kernels (profiles/r03_length_sweep.log, strided 3 GB
+// batches): 2 below 1 KiB, 4 below 2 KiB (k_frames_carry), 8 below 48 KiB,
+// 16 above. G = 8 from 2 KiB gained 3-5% over G = 4 on 2-4 KiB frames and
+// 5% on u4200d (profiles/r03_ab_geom_short.log). The ragged path keeps its
+// length classes (kClassLanes), whose buckets are rounds of their class.
 uint32_t lanes_per_frame(uint32_t len)
 {
     const uint32_t f = forced_lanes();
-    return f ? f : (uint32_t)class_lanes(length_class(len));
+    if (f) return f;
+    return len < 1024u ? 2u : len < 2048u ? 4u : len < 49152u ? 8u : 16u;
 }
 
 // G for a uniform batch of n frames of len bytes: the class's G, doubled while
