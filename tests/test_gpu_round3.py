@@ -1,10 +1,11 @@
 """GPU parity of this round's kernel paths, through the C ABI against the
 oracle (bit-exact):
-  * k_frames_carry (uniform batches at G <= 4: the next group's rounds 0 and 1
-    issued during this group's last round, unit 0 read inside its frame's
-    first line): descriptor batches in shuffled memory order, frames at the
-    very start of the buffer, every start alignment, header_crc and verify,
-    and a batch long enough for the dynamic-tail queue (two-ahead dequeue);
+  * unit 0 read inside its frame's first line (four dwordx4 loads and a select
+    network) at G = 2 and 4: descriptor batches in shuffled memory order,
+    frames at the very start of the buffer, every start alignment, header_crc
+    and verify, and a batch long enough for the dynamic-tail queue (these
+    tests were written for the carried-frames kernel, measured and removed
+    this round; they pin the same paths of k_frames);
   * the ragged path's single-bucket batches (k_bin_scatter skips the scatter,
     the kernel takes frame i at sorted position i), alternated with
     multi-bucket batches on the same stream (scratch state carried between
@@ -67,8 +68,8 @@ def _frames(vc, dev, base, offs, lens, hint, header=True):
 
 
 @pytest.mark.parametrize("L", [60, 64, 65, 127, 128, 129, 600, 1023, 1100, 4200, 8191])
-def test_carry_shuffled_descriptors(vc, dev, L):
-    vc.set_geometry()  # the measured geometry: G = 2 or 4 below 8 KiB -> k_frames_carry
+def test_short_shuffled_descriptors(vc, dev, L):
+    vc.set_geometry()  # the measured geometry: G = 2, 4 or 8 below 8 KiB
     base, offs, lens = _shuffled(1000 + L, 3000, L)
     got, got_h = _frames(vc, dev, base, offs, lens, hint=L)
     want, want_h = _oracle.frames(base, offs, lens, header=True)
@@ -78,7 +79,7 @@ def test_carry_shuffled_descriptors(vc, dev, L):
 
 @pytest.mark.parametrize("G", [2, 4])
 @pytest.mark.parametrize("shift", range(8))
-def test_carry_every_start_alignment(vc, dev, G, shift):
+def test_short_every_start_alignment(vc, dev, G, shift):
     # frames at byte offsets shift, shift + stride, ... with the first frame
     # near the buffer start: unit 0 starts before the buffer for small shifts
     vc.set_geometry(G, 1)
@@ -95,7 +96,7 @@ def test_carry_every_start_alignment(vc, dev, G, shift):
     vc.set_geometry()
 
 
-def test_carry_verify_detects_corruption(vc, dev):
+def test_short_verify_detects_corruption(vc, dev):
     vc.set_geometry()
     base, offs, lens = _shuffled(3001, 5000, 1100)
     crc = _oracle.frames(base, offs, lens)
@@ -111,7 +112,7 @@ def test_carry_verify_detects_corruption(vc, dev):
     assert set(np.flatnonzero(ok.cpu().numpy() == 0).tolist()) == set(bad.tolist())
 
 
-def test_carry_dynamic_tail_every_frame(vc, dev):
+def test_short_dynamic_tail_every_frame(vc, dev):
     # long enough for the partitioned dynamic-tail queue (>= 4 group rounds of
     # 16 KiB+ descriptor groups): 300,000 x 1,100 B, strided and descriptor,
     # twice on one stream (the last wave out re-zeroes the queue)

@@ -104,14 +104,16 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
 // Unit 0 through its frame's first line. Unit 0 starts pad bytes before the
 // frame, so read whole it can reach into the previous 128-B line (the previous
 // frame's end, which that frame reads a group-time later: 1,100-B frames read
-// 1.30x their bytes that way, against 1.12x with clamped loads). Sixteen
-// clamped dword loads need sixteen live addresses, which spilled in the last
-// round. Here the 64 B are read from A = max(unit start, the frame's first
-// line) by four dwordx4 loads, never outside that line (A is dword-aligned and
-// A + 64 stays in the line), and moved up by the s = (A - unit start) / 4
-// words skipped: a four-stage select network. The words before the frame are
-// masked later (unit0_finish). A line never crosses a page, so the read is
-// safe even for a frame at the very start of its buffer.
+// 1.30x their bytes that way, against 1.12x when only the frame's own line is
+// touched). Sixteen clamped dword loads (round 2) issued sixteen memory
+// instructions and needed sixteen addresses. Here the 64 B are read from
+// A = max(unit start, the frame's first line) by four dwordx4 loads, never
+// outside that line (A is dword-aligned and A + 64 stays in the line), and
+// moved up by the s = (A - unit start) / 4 words skipped: a four-stage select
+// network. The words before the frame are masked later (unit0_finish). A line
+// never crosses a page, so the read is safe even for a frame at the very start
+// of its buffer. (Uniform 1,100-B ragged batches +3.5%, cfg5 +0.9%:
+// profiles/r03_ab_unit0_line.log.)
 // (The loads are issued by load_unit0_line, the words moved by
 // unit0_line_shift where they are used: the shift amount is recomputed, so
 // nothing extra stays live in between.)
@@ -439,145 +441,6 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     return acc;  // lane G - 1: the frame's raw register (before xorout)
 }
 
-// ---- carried frames (k_frames_carry): the next group's rounds 0 and 1 are
-// issued during this group's last round ----------------------------------------
-// hash_frame issues a frame's round-0 and round-1 loads when its hashing
-// starts, so nothing of a wave is in flight while the previous group's last
-// round, merge and outputs run: one exposed memory latency per group, a large
-// share of a short frame's 5 rounds. Here the caller passes the frame's
-// round 0 (w0) and round 1 (nxt) already in flight, and during the frame's
-// last round next(w0, nxt) issues the next frame's (after this frame's end
-// loads, which loads complete in order behind). A third 16-word buffer is
-// live in the last round, which fits the register budget at G <= 4.
-// A lane's view of a frame on the unit grid (inactive lanes: L = 0, R = 0).
-struct Geo {
-    gu8 *fp;
-    uint32_t L, tb, Lg, U, R, pad;
-    int u0;  // the lane's unit in round 0 (may be negative)
-};
-
-__device__ __forceinline__ Geo frame_geo(const uint8_t *base, uint64_t off, uint32_t L, bool active, int g, int G, int lgG)
-{
-    Geo q;
-    q.fp = gptr(base) + off;
-    q.L = L;
-    q.tb = min((uint32_t)((uintptr_t)(q.fp + L) & 3u), L);
-    q.Lg = L - q.tb;
-    q.U = q.Lg ? (q.Lg + kUnit - 1) / kUnit : 1u;
-    q.R = active ? (q.U + (uint32_t)G - 1u) >> lgG : 0u;
-    q.pad = q.U * kUnit - q.Lg;
-    q.u0 = (int)q.U - G * (int)q.R + g;
-    return q;
-}
-
-// A frame's rounds 0 (w0) and 1 (nxt, when it has one).
-__device__ __forceinline__ void load_r01(uint32_t (&w0)[kWords], uint32_t (&nxt)[kWords], const Geo &q, int G)
-{
-    if (q.u0 > 0 && q.Lg >= 4) load_full(w0, q.fp + (int64_t)q.u0 * kUnit - q.pad);
-    if (q.u0 == 0 && q.Lg >= 4) load_unit0_line(w0, q.fp, q.pad);
-    if (q.R >= 2u) load_full(nxt, q.fp + ((int64_t)q.u0 + G) * kUnit - q.pad);
-}
-
-template <int G, typename Next>
-__device__ __forceinline__ void hash_frame_carry(const FrameParams &p, uint32_t f, bool active, const Geo &q,
-                                                 uint32_t (&w0)[kWords], uint32_t (&nxt)[kWords], int g,
-                                                 const SliceBases &sb, Next &&next)
-{
-    constexpr int lgG = ilog2(G);
-    const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
-    const bool hdr = q.R > 0 && q.u0 == 0 && p.out_hdr;
-    const bool last_lane = active && g == G - 1;
-    // header words (the lane of unit 0; its line is in flight as round 0),
-    // used after the rounds
-    uint32_t h0 = 0, h1 = 0;
-    if (hdr && q.L >= 8) {
-        h0 = ld32(q.fp);
-        h1 = ld32(q.fp + 4);
-    }
-    // the frame's end loads, issued before the next frame's
-    uint32_t tail[3] = {0, 0, 0}, trailer = 0;
-    auto issue_end = [&] {
-        if (last_lane) {
-            if (q.tb && q.Lg >= 4) {
-#pragma unroll
-                for (uint32_t j = 0; j < 3; j++) tail[j] = q.fp[q.Lg + min(j, q.tb - 1)];
-            }
-            if (p.verify) trailer = ld32(q.fp + q.L);
-        }
-    };
-    int first = (q.R == 0 || q.u0 < 0) ? kWords : (q.u0 == 0 ? (int)(q.pad >> 2) : 0);
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
-    first = __builtin_amdgcn_readfirstlane(first);
-    uint32_t w[kWords];
-#pragma unroll
-    for (int i = 0; i < kWords; i++) w[i] = w0[i];
-    if (q.u0 == 0 && q.Lg >= 4) unit0_line_shift(w, q.fp, q.pad);
-    if (q.R <= 1u) {  // round 0 is the last round
-        issue_end();
-        next(w0, nxt);
-    }
-    uint32_t acc = 0;
-    if (q.R > 0) {
-        unit0_finish(w, q.u0, q.Lg, q.pad, seed);
-        acc = s4_words_from(first, w, sb);
-        if (q.u0 == 0 && q.Lg < 4) {  // tiny: the state of all L bytes straight from the seed
-            acc = seed;
-            for (uint32_t i = 0; i < q.L; i++) acc = byte_step(acc, q.fp[i], sb);
-        }
-    }
-    // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, round 1).
-    const bool seed_spill = g == 0 && q.pad > kUnit - 4 && (int)q.U - G * (int)(q.R - 1) == 1;
-    gu8 *up = q.fp + ((int64_t)q.u0 + 2 * G) * kUnit - q.pad;  // round 2
-    for (uint32_t k = 1; k < q.R; k++) {
-#pragma unroll
-        for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-        if (k + 1 < q.R) {
-            load_full(nxt, up);
-            up += (uint64_t)G * kUnit;
-        } else {
-            issue_end();
-            next(w0, nxt);
-        }
-        if (k == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - q.pad));
-        if (G > 1) acc = map_apply(acc, gap_map(lgG));
-#pragma unroll
-        for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
-    }
-    if (hdr) {
-        uint32_t h = seed;
-        if (q.L >= 8) {
-            h = s4_step(h, h0, sb);
-            h = s4_step(h, h1, sb);
-        } else {
-            for (uint32_t i = 0; i < q.L; i++) h = byte_step(h, q.fp[i], sb);
-        }
-        p.out_hdr[f] = h ^ p.xorout;
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxTree; j++) {
-        if ((1 << j) >= G) break;
-        const uint32_t other = __shfl_xor(acc, 1 << j);
-        const bool right = (g >> j) & 1;
-        const uint32_t left = right ? other : acc;
-        acc = map_apply(left, tree_map(j)) ^ (right ? acc : other);
-    }
-    if (last_lane) {
-        if (q.Lg >= 4) {
-#pragma unroll
-            for (uint32_t j = 0; j < 3; j++)
-                if (j < q.tb) acc = byte_step(acc, tail[j], sb);
-        }
-        const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc) p.out_crc[f] = crc;
-        if (p.verify) {
-            const bool good = (crc == trailer);
-            if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
-            if (!good && p.nbad) atomicAdd(p.nbad, 1u);
-        }
-    }
-}
-
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
 __device__ uint64_t g_vcrc_time[4096 * 4];
 __device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lane 0's frame in the wave's last item
@@ -700,97 +563,6 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     if (ql == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
         if (out == (uint32_t)nwaves - 1u) {  // every wave is past its last dequeue
-            for (uint32_t i = 0; i < P; i++) atomicExch(&p.qhead[i * 16u], 0u);
-            atomicExch(&p.qhead[kDynParts * 16u], 0u);
-        }
-    }
-}
-
-// k_frames with carried frames (hash_frame_carry), G <= 4, no payload states:
-// the same group deal and dynamic tail as k_frames, walked one group ahead.
-// While group A hashes, group B's descriptors are in flight, and B's rounds
-// 0 and 1 are issued during A's last round. A queue dequeue is issued two
-// groups ahead (its result is needed only when A is done), so no atomic's
-// latency sits in front of a group.
-template <int G>
-__global__ __launch_bounds__(kBlock) void k_frames_carry(const FrameParams p)
-{
-    VCRC_STAMP(0);
-    VCRC_KARG_EARLY("s"(p.consts), "s"(p.base), "s"(p.off), "s"(p.len), "s"(p.stride), "s"(p.flen), "s"(p.last_len),
-                    "s"(p.n), "s"(p.seed0), "s"(p.seed_rest), "s"(gridDim.x));
-    constexpr int kGroups = 64 / G, lgG = ilog2(G);
-    constexpr uint64_t kNone = ~0ull;
-    const int lane = threadIdx.x & 63, g = lane & (G - 1), slot = lane >> lgG;
-    const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
-    // wave-uniform group indices (readfirstlane: SGPRs); frame indices fit in 32 bits (n is a u32)
-    const uint64_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t S = nwaves * kGroups;  // frames per static group round
-    LdsImage im;
-    lds_tables_issue(p.consts, im);
-    // Group sequence: static groups wave * kGroups + k * S below dyn, then (with
-    // a queue) groups dyn + (part + P * k) * kGroups pulled from partition part.
-    const uint64_t dyn = p.qhead ? (uint64_t)p.static_rounds * S : kNone;
-    const uint32_t P = p.qhead ? min(min(p.qparts, kDynParts), gridDim.x) : 1u, part = blockIdx.x % P;
-    auto dequeue = [&]() -> uint32_t {
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
-        return k;
-    };
-    auto dyn_group = [&](uint32_t k) -> uint64_t {
-        const uint64_t gq = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(k)) * kGroups;
-        return gq < p.n ? gq : kNone;
-    };
-    // successor of group x: static, or (deq) from the queue, or none
-    auto succ = [&](uint64_t x, bool &deq) -> uint64_t {
-        deq = false;
-        if (x == kNone) return kNone;
-        const uint64_t s = x + S;
-        if (x < dyn && s < dyn && s < p.n) return s;
-        deq = p.qhead != nullptr;
-        return kNone;
-    };
-    const uint64_t ga = wave * kGroups;
-    uint32_t fa = (uint32_t)ga + (uint32_t)slot;
-    uint64_t offa = 0;
-    uint32_t La = 0;
-    bool acta = ga + (uint64_t)slot < p.n;
-    if (acta) frame_desc(p, fa, offa, La);
-    uint32_t w0[kWords], nxt[kWords];
-    load_r01(w0, nxt, frame_geo(p.base, offa, La, acta, g, G, lgG), G);
-    // the LDS fill and the barrier run under the first frame's memory latency
-    lds_tables_write(im);
-    __syncthreads();
-    VCRC_STAMP(1);
-    if (ga < p.n) {
-        bool deq;
-        uint64_t gb = succ(ga, deq);
-        if (deq) gb = dyn_group(dequeue());  // only when a wave has a single static group
-        for (;;) {
-            const uint32_t fb = (uint32_t)gb + (uint32_t)slot;
-            uint64_t offb = 0;
-            uint32_t Lb = 0;
-            const bool actb = gb != kNone && gb + (uint64_t)slot < p.n;
-            if (actb) frame_desc(p, fb, offb, Lb);
-            bool deq_c;
-            const uint64_t gc = succ(gb, deq_c);
-            const uint32_t kc = deq_c ? dequeue() : 0u;
-            hash_frame_carry<G>(p, fa, acta, frame_geo(p.base, offa, La, acta, g, G, lgG), w0, nxt, g, sb,
-                                [&](uint32_t(&a)[kWords], uint32_t(&b)[kWords]) {
-                                    load_r01(a, b, frame_geo(p.base, offb, Lb, actb, g, G, lgG), G);
-                                });
-            if (gb == kNone) break;
-            fa = fb;
-            offa = offb;
-            La = Lb;
-            acta = actb;
-            gb = deq_c ? dyn_group(kc) : gc;
-        }
-    }
-    VCRC_STAMP(2);
-    if (p.qhead && lane == 0) {  // every wave ends on a failed dequeue; the last one out re-zeroes the heads
-        const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
-        if (out == (uint32_t)nwaves - 1u) {
             for (uint32_t i = 0; i < P; i++) atomicExch(&p.qhead[i * 16u], 0u);
             atomicExch(&p.qhead[kDynParts * 16u], 0u);
         }

@@ -243,7 +243,7 @@ uint32_t forced_lanes()
 
 // Lanes that share one frame (G) in uniform batches, by length: the measured
 // best of the current kernels (profiles/r03_length_sweep.log, strided 3 GB
-// batches): 2 below 1 KiB, 4 below 2 KiB (k_frames_carry), 8 below 48 KiB,
+// batches): 2 below 1 KiB, 4 below 2 KiB, 8 below 48 KiB,
 // 16 above. G = 8 from 2 KiB gained 3-5% over G = 4 on 2-4 KiB frames and
 // 5% on u4200d (profiles/r03_ab_geom_short.log). The ragged path keeps its
 // length classes (kClassLanes), whose buckets are rounds of their class.
@@ -294,30 +294,12 @@ int prefetch_depth()
     return forced >= 0 ? forced : 1;
 }
 
-// Carried frames (k_frames_carry: the next group's first loads issued during
-// this group's last round) at G <= 4 and the default depth, payload states
-// excepted: VAL_GPU_CARRY=0 (or -DVCRC_CARRY_DEFAULT=0) selects k_frames<G, 1>.
-#ifndef VCRC_CARRY_DEFAULT
-#define VCRC_CARRY_DEFAULT 1
-#endif
-bool carry_enabled()
-{
-    static const bool on = getenv("VAL_GPU_CARRY") ? atoi(getenv("VAL_GPU_CARRY")) != 0 : VCRC_CARRY_DEFAULT != 0;
-    return on;
-}
-
 template <int G>
 void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
 {
     if (p.out_pay) {  // payload states: the default depth only
         hipLaunchKernelGGL((k_frames<G, 1, true>), grid, dim3(kBlock), 0, s, p);
         return;
-    }
-    if constexpr (G >= 2 && G <= 4) {
-        if (pf == 1 && carry_enabled()) {
-            hipLaunchKernelGGL((k_frames_carry<G>), grid, dim3(kBlock), 0, s, p);
-            return;
-        }
     }
     switch (pf) {
     case 0: hipLaunchKernelGGL((k_frames<G, 0, false>), grid, dim3(kBlock), 0, s, p); break;
