@@ -77,7 +77,6 @@ struct FrameParams {
     uint32_t *qhead;         // uniform mode: dynamic-tail queue, kDynQueueBytes (zero on entry, re-zeroed), nullable
     uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
     uint32_t qparts;         // with qhead: queue partitions, 1..kDynParts
-    uint32_t r0x4;           // uniform batches: whole round-0 units by dwordx4 (load_unit0)
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -141,52 +140,53 @@ __device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp,
 // Words of a lane's round-0 unit u: u > 0 a full unit; u == 0 the front-padded
 // first unit, with the seed in frame bytes 0..3; u < 0 nothing. Lg = bytes on
 // the unit grid; Lg < 4 frames take the byte path (tiny). Loads only, into
-// registers left undefined for lanes without a unit; the masks and the seed
-// are applied by unit0_finish where the words are first used. hipcc waits for
-// every outstanding load at the first use of a loaded value, and at the end
-// of a branch whose loads feed a value defined on the other path too: with
-// the masks next to the loads (and zeros on the other path) the 16 loads of
-// unit 0 ran one memory round trip after another, behind round 1's prefetch.
+// registers left undefined for lanes without a unit; unit 0's words are moved
+// into place (unit0_line_shift) and the masks and the seed applied
+// (unit0_finish) where the words are first used. hipcc waits for every
+// outstanding load at the first use of a loaded value, and at the end of a
+// branch whose loads feed a value defined on the other path too: with the
+// masks next to the loads (and zeros on the other path) the loads of unit 0
+// ran one memory round trip after another, behind round 1's prefetch.
 // Unit u starts at fp + 64u - pad, dword-aligned (the grid ends at
-// floor4(frame end)). Unit 0 starts pad bytes before the frame: a word of it
-// wholly before the frame reads the frame's first dword, base + (pad & ~3),
-// instead (no byte outside that dword is touched) and is masked to zero.
-// The loads are issued by every lane, branch-free: a lane without a unit
-// reads 64 B of `dummy` (the constant blob, an L1/L2 hit) instead. Behind a
-// skippable branch, the waitcnt pass could not count them, and the prologue's
-// waits for the constant-blob loads (issued first) then also waited for most
-// of the frame loads: the LDS fill stopped overlapping the first memory
-// latency (region launches: prologue 7.7 us; tools/timing_region.py).
-// BF (k_region): branch-free, every lane issues the loads.
-// Otherwise (k_frames): only lanes with a unit issue them; measured faster on
-// frame batches (the dummy loads cost cfg2 3%, a 256-frame window 9%).
-// r0x4 (k_frames, uniform batches whose round 0 is at least half full): the
-// lanes holding a whole unit read it by dwordx4 as in k_region (2048 x 64 KiB
-// windows 39.7 -> 35.6 us; cfg2, whose round 0 holds unit 0 alone, -1.3% with
-// it: profiles/r02_ab_r0x4.log).
-template <bool BF>
-__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad, gu8 *dummy,
-                                           bool r0x4)
+// floor4(frame end)); unit 0 is read from inside the frame's first line
+// (load_unit0_line). Every round-0 unit is read by four dwordx4 loads: one
+// load shape on every path. With two shapes (round 2: sixteen clamped dword
+// loads for unit 0 beside whole-unit loads; round 3 briefly: the line loads
+// beside them) the results met in copies at the join, which waited for the
+// loads there, and the LDS fill stopped overlapping the first memory latency
+// (one-pass windows of 64-1024 frames +1.7 us per call,
+// profiles/r03_ab_round0_shape.log).
+// BF (k_region, k_frames_split): branch-free, every lane issues the loads; a
+// lane without a unit reads 64 B of `dummy` (the constant blob, an L1/L2
+// hit). Behind a skippable branch, the waitcnt pass could not count them, and
+// the prologue's waits for the constant-blob loads (issued first) then also
+// waited for most of the frame loads (region launches: prologue 7.7 us;
+// tools/timing_region.py).
+// Otherwise (k_frames, ragged): only lanes with a unit issue them; measured
+// faster on frame batches (the dummy loads cost cfg2 3%, a 256-frame window 9%).
+// C0 (k_frames launches that are one pass of the grid: windows, cfg2): round
+// 2's sixteen dword loads per round-0 unit, unit 0's clamped to the frame's
+// first dword (a word wholly before the frame reads that dword and is masked
+// to zero). The line loads above are faster on batches of many group rounds
+// (1,100-B frames +4-7%) and slower on one-pass launches, where round 0 is the
+// whole wait (windows of 64-1024 frames -10%, cfg2 -3.4%;
+// profiles/r03_ab_round0_shape.log), so both are kept and the host picks.
+template <bool BF, bool C0 = false>
+__device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp, uint32_t Lg, uint32_t pad, gu8 *dummy)
 {
     const bool has = u >= 0 && Lg >= 4;
-    if (!BF && has && u == 0) {  // k_frames, ragged: four dwordx4 loads inside the frame's first line
-        load_unit0_line(w, fp, pad);
-        return;
-    }
-    if (BF || has) {
-        gu8 *base = has ? fp + ((int64_t)u * kUnit - pad) : dummy;
-        const uint32_t lo = (has && u == 0) ? (pad & ~3u) : 0u;
-        if (lo == 0 && (BF || (r0x4 && u > 0))) {
-            // k_region: every unit but the window's first is whole, so four
-            // dwordx4 loads instead of sixteen dword loads: 8 MiB windows
-            // 15.9 -> 10.9 us. In k_frames round 0 mostly holds unit 0 alone
-            // and the same change measured neutral (profiles/r02_ab_region_x4.log)
-            load_full(w, base);
-        } else {
+    if (C0 && !BF) {
+        if (has) {
+            gu8 *const base = fp + ((int64_t)u * kUnit - pad);
+            const uint32_t lo = u == 0 ? (pad & ~3u) : 0u;
 #pragma unroll
             for (int i = 0; i < kWords; i++) w[i] = *reinterpret_cast<gu32 *>(base + max(4u * (uint32_t)i, lo));
         }
+        return;
     }
+    gu8 *const at = fp + ((int64_t)u * kUnit - pad) + (u == 0 ? unit0_line_skip(fp, pad) : 0u);
+    if (BF) load_full(w, has ? at : dummy);
+    else if (has) load_full(w, at);
 }
 
 // Mask and seed of unit-0 word i (frame offset q = 4i - pad): bytes before the
@@ -275,7 +275,7 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 struct NoMid {
     __device__ void operator()() const {}
 };
-template <int GT, int PF, bool PAY, bool BF, typename Pre, typename Mid = NoMid>
+template <int GT, int PF, bool PAY, bool BF, bool C0 = false, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
@@ -300,7 +300,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     uint32_t w0[kWords];
     const bool tiny = u0 == 0 && Lg < 4;
     gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
-    load_unit0<BF>(w0, u0, fp, Lg, pad, dummy, p.r0x4 != 0);
+    load_unit0<BF, C0>(w0, u0, fp, Lg, pad, dummy);
     // header_crc: by the lane holding unit 0, from the frame's first line,
     // which round 0 reads anyway (read after the merge, the line had left the
     // caches: +0.4% HBM traffic on cfg3).
@@ -340,7 +340,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
-        if (!BF && u0 == 0 && Lg >= 4) unit0_line_shift(w0, fp, pad);
+        if (u0 == 0 && Lg >= 4 && (BF || !C0)) unit0_line_shift(w0, fp, pad);
         unit0_finish(w0, u0, Lg, pad, seed);
         acc = s4_words_from(first, w0, sb);
         if (tiny) {  // Lg < 4: state of all L bytes straight from the seed
@@ -476,7 +476,7 @@ __device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lan
 // the static deal is kept.
 // One frame group of a uniform wave: hash group f.., fetch the next group's
 // descriptors meanwhile, advance.
-template <int G, int PF, bool PAY, typename Pre>
+template <int G, int PF, bool PAY, bool C0, typename Pre>
 __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
                                            uint64_t step, int lane, const SliceBases &sb, Pre &&pre)
 {
@@ -484,14 +484,14 @@ __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, ui
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    hash_frame<G, PF, PAY, false>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
+    hash_frame<G, PF, PAY, false, C0>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
     f = fn;
     off = off_n;
     L = L_n;
     fb += step;
 }
 
-template <int G, int PF, bool PAY>
+template <int G, int PF, bool PAY, bool C0 = false>
 __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
 {
     VCRC_STAMP(0);
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loop.
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
-    group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
+    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         VCRC_STAMP(1);
     });
     if (!p.qhead) {
-        while (fb < p.n) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
         VCRC_STAMP(2);
         return;
     }
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // groups keep one word, which evens the end out better. The last wave out
     // re-zeroes the heads for the next launch on this stream.
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
-    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
     const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
     // the lane id again from mbcnt: kept live from the entry, it was the one
     // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         uint64_t od = 0;
         uint32_t Ld = 0;
         if (fd < p.n) frame_desc(p, fd, od, Ld);
-        hash_frame<G, PF, PAY, false>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
+        hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
     }
     VCRC_STAMP(2);
     if (ql == 0) {

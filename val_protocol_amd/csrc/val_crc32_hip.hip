@@ -294,11 +294,17 @@ int prefetch_depth()
     return forced >= 0 ? forced : 1;
 }
 
+// one_pass: every wave hashes at most one frame group (windows, cfg2): round
+// 0's units by dword loads (k_frames C0; crc_kernels.hpp load_unit0).
 template <int G>
-void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p)
+void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p, bool one_pass)
 {
     if (p.out_pay) {  // payload states: the default depth only
         hipLaunchKernelGGL((k_frames<G, 1, true>), grid, dim3(kBlock), 0, s, p);
+        return;
+    }
+    if (pf == 1 && one_pass) {
+        hipLaunchKernelGGL((k_frames<G, 1, false, true>), grid, dim3(kBlock), 0, s, p);
         return;
     }
     switch (pf) {
@@ -420,19 +426,15 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
 #endif
         p.static_rounds = (uint32_t)(VCRC_DYN_DIV == 1 ? 1u : rounds - std::max<uint64_t>(1, rounds / VCRC_DYN_DIV));
     }
-    {  // round 0 of a typical frame at least half full: its whole units by dwordx4
-        const uint64_t U = std::max<uint64_t>(1, ((uint64_t)len + kUnit - 1) / kUnit);
-        const uint64_t r0 = U - (uint64_t)G * ((U + G - 1) / G - 1);
-        p.r0x4 = r0 * 2 >= G ? 1u : 0u;
-    }
+    const bool one_pass = ((uint64_t)p.n + 64 / G - 1) / (64 / G) <= (uint64_t)grid.x * kWavesPerBlock;
     switch (G) {
-    case 1: launch_uniform_g<1>(pf, grid, s, p); break;
-    case 2: launch_uniform_g<2>(pf, grid, s, p); break;
-    case 4: launch_uniform_g<4>(pf, grid, s, p); break;
-    case 8: launch_uniform_g<8>(pf, grid, s, p); break;
-    case 16: launch_uniform_g<16>(pf, grid, s, p); break;
-    case 32: launch_uniform_g<32>(pf, grid, s, p); break;
-    case 64: launch_uniform_g<64>(pf, grid, s, p); break;
+    case 1: launch_uniform_g<1>(pf, grid, s, p, one_pass); break;
+    case 2: launch_uniform_g<2>(pf, grid, s, p, one_pass); break;
+    case 4: launch_uniform_g<4>(pf, grid, s, p, one_pass); break;
+    case 8: launch_uniform_g<8>(pf, grid, s, p, one_pass); break;
+    case 16: launch_uniform_g<16>(pf, grid, s, p, one_pass); break;
+    case 32: launch_uniform_g<32>(pf, grid, s, p, one_pass); break;
+    case 64: launch_uniform_g<64>(pf, grid, s, p, one_pass); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(hipGetLastError(), "k_frames launch");
