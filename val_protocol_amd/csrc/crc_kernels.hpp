@@ -113,17 +113,13 @@ __device__ __forceinline__ void load_full(uint32_t (&w)[kWords], gu8 *up)
 // never crosses a page, so the read is safe even for a frame at the very start
 // of its buffer. (Uniform 1,100-B ragged batches +3.5%, cfg5 +0.9%:
 // profiles/r03_ab_unit0_line.log.)
-// (The loads are issued by load_unit0_line, the words moved by
-// unit0_line_shift where they are used: the shift amount is recomputed, so
-// nothing extra stays live in between.)
+// (The loads are issued by load_unit0, the words moved by unit0_line_shift
+// where they are used: the shift amount is recomputed, so nothing extra stays
+// live in between.)
 __device__ __forceinline__ uint32_t unit0_line_skip(gu8 *fp, uint32_t pad)  // bytes of unit 0 before fp's line
 {
     const uint32_t in_line = (uint32_t)((uintptr_t)fp & 127u);
     return pad > in_line ? pad - in_line : 0u;
-}
-__device__ __forceinline__ void load_unit0_line(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
-{
-    load_full(w, fp - pad + unit0_line_skip(fp, pad));
 }
 __device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp, uint32_t pad)
 {
@@ -149,7 +145,7 @@ __device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp,
 // ran one memory round trip after another, behind round 1's prefetch.
 // Unit u starts at fp + 64u - pad, dword-aligned (the grid ends at
 // floor4(frame end)); unit 0 is read from inside the frame's first line
-// (load_unit0_line). Every round-0 unit is read by four dwordx4 loads: one
+// (unit0_line_skip). Every round-0 unit is read by four dwordx4 loads: one
 // load shape on every path. With two shapes (round 2: sixteen clamped dword
 // loads for unit 0 beside whole-unit loads; round 3 briefly: the line loads
 // beside them) the results met in copies at the join, which waited for the
@@ -158,7 +154,9 @@ __device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp,
 // profiles/r03_ab_round0_shape.log).
 // BF (k_region, k_frames_split): branch-free, every lane issues the loads; a
 // lane without a unit reads 64 B of `dummy` (the constant blob, an L1/L2
-// hit). Behind a skippable branch, the waitcnt pass could not count them, and
+// hit); whole units by dwordx4, the window's unit 0 by clamped dword loads
+// (the line loads cost these one-pass launches about 2 us per call:
+// profiles/r03_summary.json ab_region). Behind a skippable branch, the waitcnt pass could not count them, and
 // the prologue's waits for the constant-blob loads (issued first) then also
 // waited for most of the frame loads (region launches: prologue 7.7 us;
 // tools/timing_region.py).
@@ -184,9 +182,18 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp
         }
         return;
     }
-    gu8 *const at = fp + ((int64_t)u * kUnit - pad) + (u == 0 ? unit0_line_skip(fp, pad) : 0u);
-    if (BF) load_full(w, has ? at : dummy);
-    else if (has) load_full(w, at);
+    if (BF) {  // k_region, k_frames_split: every unit but a window's first is whole
+        gu8 *const base = has ? fp + ((int64_t)u * kUnit - pad) : dummy;
+        const uint32_t lo = (has && u == 0) ? (pad & ~3u) : 0u;
+        if (lo == 0) {
+            load_full(w, base);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kWords; i++) w[i] = *reinterpret_cast<gu32 *>(base + max(4u * (uint32_t)i, lo));
+        }
+        return;
+    }
+    if (has) load_full(w, fp + ((int64_t)u * kUnit - pad) + (u == 0 ? unit0_line_skip(fp, pad) : 0u));
 }
 
 // Mask and seed of unit-0 word i (frame offset q = 4i - pad): bytes before the
@@ -340,7 +347,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     if (R > 0) {
         // Round 0 alone can hold unit 0 (padding, seed, tiny frames) or no
         // unit; the register is still zero, so no gap step.
-        if (u0 == 0 && Lg >= 4 && (BF || !C0)) unit0_line_shift(w0, fp, pad);
+        if (u0 == 0 && Lg >= 4 && !BF && !C0) unit0_line_shift(w0, fp, pad);
         unit0_finish(w0, u0, Lg, pad, seed);
         acc = s4_words_from(first, w0, sb);
         if (tiny) {  // Lg < 4: state of all L bytes straight from the seed
