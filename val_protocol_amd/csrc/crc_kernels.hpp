@@ -145,8 +145,9 @@ __device__ __forceinline__ void unit0_line_shift(uint32_t (&w)[kWords], gu8 *fp,
 // ran one memory round trip after another, behind round 1's prefetch.
 // Unit u starts at fp + 64u - pad, dword-aligned (the grid ends at
 // floor4(frame end)); unit 0 is read from inside the frame's first line
-// (unit0_line_skip). Every round-0 unit is read by four dwordx4 loads: one
-// load shape on every path. With two shapes (round 2: sixteen clamped dword
+// (unit0_line_skip). In k_frames (multi-pass launches) and the ragged kernel
+// every round-0 unit is read by four dwordx4 loads: one load shape on every
+// path. With two shapes (round 2: sixteen clamped dword
 // loads for unit 0 beside whole-unit loads; round 3 briefly: the line loads
 // beside them) the results met in copies at the join, which waited for the
 // loads there, and the LDS fill stopped overlapping the first memory latency
