@@ -63,7 +63,9 @@ def kernel_trace(o, sub, rnd, tag):
     top = max(csv.DictReader(open(stats)), key=lambda r: float(r["TotalDurationNs"]))
     main = [r for r in crc if r["Kernel_Name"] == top["Name"]]
     steps = int(os.environ.get("BENCH_STEPS", "20"))  # bench.py's timed steps (default 20, after 15 warmup)
-    last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in main[-steps:]]
+    extra = min(steps, 5)  # bench.py's untimed per-step pass after the timed region (round 3 on)
+    timed = main[-(steps + extra):-extra] if len(main) >= steps + extra else main[-steps:]
+    last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     return {"kernel": top["Name"], "dispatches": int(top["Calls"]), "avg_ms_all_dispatches": float(top["AverageNs"]) / 1e6,
             "timed_dispatches": len(last),
             "avg_ms_timed_region": sum(last) / len(last) / 1e6 if last else None}
