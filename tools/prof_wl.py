@@ -2,7 +2,8 @@
 """Profiling target for rocprofv3 passes over the A/B workloads of
 tools/ab_libs.py (u1100d, s1100, cfg3b, cfg5log, ...): builds the workload
 once, launches the frames kernel `reps` times through the product library.
-Usage: prof_wl.py WORKLOAD [reps]  (tooling only)"""
+Usage: prof_wl.py WORKLOAD [reps]  (tooling only; PROF_LIB=path profiles
+another build of the library, e.g. build/libval_B.so)"""
 import os
 import sys
 
@@ -12,6 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import val_protocol_amd.crc as vc  # noqa: E402
 from tools.ab_libs import workload  # noqa: E402
 
+if os.environ.get("PROF_LIB"):
+    vc.LIB_PATH = os.path.abspath(os.environ["PROF_LIB"])
 name = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda:0")
