@@ -554,18 +554,50 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // the lane id again from mbcnt: kept live from the entry, it was the one
     // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
     // launch later)
+    // Short groups (P > 1 partitions), one group ahead: each group's dequeue is
+    // issued when the previous group starts, and its descriptors are fetched once that group's round 0 is
+    // hashed (the mid() hook, as the ragged kernel does), so a group's first
+    // loads no longer wait for an atomic and then for its descriptors: two
+    // dependent round trips per group, which short groups (1,100-B frames:
+    // five rounds) could not hide (u1100d +3.0-3.7%, profiles/r03_ab_dyn_one_ahead_gated.log).
+    // Every wave still ends on one failed dequeue, so the exit count below is
+    // unchanged.
     const int ql = (int)__lane_id();
-    for (;;) {
-        uint32_t k = 0;
-        if (ql == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
-        k = __builtin_amdgcn_readfirstlane(k);
-        const uint64_t gb = dyn + ((uint64_t)part + (uint64_t)P * k) * kGroups;
-        if (gb >= p.n) break;
-        const uint64_t fd = gb + (uint64_t)(ql / G);
-        uint64_t od = 0;
-        uint32_t Ld = 0;
-        if (fd < p.n) frame_desc(p, fd, od, Ld);
-        hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
+    if (P == 1u) {  // long groups: dequeue at each group's start (one ahead lost cfg4 2.5%, cfg3 0.7%: a wave
+                    // then holds a reserved long group while others run dry)
+        for (;;) {
+            uint32_t k = 0;
+            if (ql == 0) k = atomicAdd(&p.qhead[0], 1u);
+            k = __builtin_amdgcn_readfirstlane(k);
+            const uint64_t gb = dyn + (uint64_t)k * kGroups;
+            if (gb >= p.n) break;
+            const uint64_t fd = gb + (uint64_t)(ql / G);
+            uint64_t od = 0;
+            uint32_t Ld = 0;
+            if (fd < p.n) frame_desc(p, fd, od, Ld);
+            hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
+        }
+    }
+    uint32_t k = 0;
+    if (P > 1u && ql == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
+    uint64_t gb = P == 1u ? p.n : dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(k)) * kGroups;
+    uint64_t fd = gb + (uint64_t)(ql / G), od = 0;
+    uint32_t Ld = 0;
+    if (fd < p.n) frame_desc(p, fd, od, Ld);
+    while (gb < p.n) {
+        uint32_t kn = 0;
+        if (ql == 0) kn = atomicAdd(&p.qhead[part * 16u], 1u);
+        uint64_t gb_n = 0, fd_n = 0, od_n = 0;
+        uint32_t Ld_n = 0;
+        hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {}, [&] {
+            gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
+            fd_n = gb_n + (uint64_t)(ql / G);
+            if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
+        });
+        gb = gb_n;
+        fd = fd_n;
+        od = od_n;
+        Ld = Ld_n;
     }
     VCRC_STAMP(2);
     if (ql == 0) {
