@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--host-inclusive", action="store_true", help="also time H2D+kernel+D2H (stderr)")
     ap.add_argument("--sort-frames", action="store_true", help="cfg5: order descriptors by length (diagnostic)")
+    ap.add_argument("--no-cfg4-strong", action="store_true",
+                    help="skip the cfg4 strong-scaling block (BASELINE configs[3]) timed after the headline")
     return ap.parse_args()
 
 
@@ -102,6 +104,36 @@ def make_ragged_frames(torch, dev, n, seed):
     idx = (d_off[ex][:, None] + 8 + torch.arange(8, device=dev)[None, :]).reshape(-1)
     buf[idx] = torch.from_numpy(file_off[ex].astype("<i8").view(np.uint8)).to(dev)
     return buf, d_off, torch.from_numpy(crc_len.astype(np.int32)).to(dev)
+
+
+def effective_cpus() -> tuple[int, int]:
+    """(CPUs this process may run on, CPUs its cgroup quota pays for): the
+    affinity set, and ceil(quota / period) from cgroup v2 cpu.max (v1:
+    cpu.cfs_quota_us / cpu.cfs_period_us) when a quota is set. A GPU box
+    shows every CPU of the machine in its affinity set but grants one GPU's
+    share (16) through the quota."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    eff = visible if quota is None else max(1, min(visible, int(-(-quota // 1))))
+    return visible, eff
 
 
 def cpu_model() -> str:
@@ -214,47 +246,22 @@ def read_roof(torch, flat, stream):
     return nbytes / (float(np.median(ms)) * 1e-3) / 1e9
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
-    gpu = local % max(ndev, 1)  # == local on a full node; lets a 1-GPU box rehearse N ranks
-    backend = os.environ.get("VAL_BENCH_BACKEND", "nccl")
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device(f"cuda:{gpu}")
-    torch.cuda.set_device(dev)
-
-    import val_protocol_amd.crc as vc
-
-    vc.init(gpu)
-    n, payload, explicit, header = CONFIGS[args.config]
-    # cfg4 is one 8 GiB file sharded across the ranks (BASELINE configs[3]):
-    # contiguous frame ranges, no collective on the data path -> strong
-    # scaling. The other configs give every rank its own batch -> weak.
-    strong = args.config == "cfg4"
+def build_workload(torch, dev, config, rank, world, verify, vc):
+    """Frames of `config` for this rank, resident in HBM. cfg4 is one 8 GiB
+    file sharded across the ranks (BASELINE configs[3]): contiguous frame
+    ranges balanced by bytes, no collective on the data path (strong
+    scaling); the other configs give every rank its own batch (weak)."""
+    n, payload, explicit, header = CONFIGS[config]
+    strong = config == "cfg4"
     n_total, first = n, rank * n
     if strong:
         from val_protocol_amd.shard import shard_frames
 
         first, n = shard_frames(n_total, world, rank)
-    ragged = args.config == "cfg5"
+    ragged = config == "cfg5"
     d_off = d_len = None
     if ragged:
         buf, d_off, d_len = make_ragged_frames(torch, dev, n, seed=1234 + rank)
-        if args.sort_frames:
-            perm = torch.argsort(d_len)
-            d_off, d_len = d_off[perm].contiguous(), d_len[perm].contiguous()
         flen, stride = 0, 0
         flat = buf
         len_hint = 0  # mixed lengths: the library bins frames by length class on the device
@@ -272,20 +279,194 @@ def main():
                 content = last_pay + (8 if explicit else 0)
                 buf[n - 1, 2], buf[n - 1, 3] = content & 0xFF, content >> 8
                 d_len[n - 1] = 8 + content
-    crc = torch.empty(n, dtype=torch.int32, device=dev)
-    hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
-    ok = torch.empty(n, dtype=torch.uint8, device=dev)
-    pay = torch.empty(n, dtype=torch.int32, device=dev) if args.pay else None
-    nbad = torch.zeros(1, dtype=torch.int32, device=dev)
     desc = ragged or strong
     kw = dict(off=d_off, length=d_len, n=n, len_hint=len_hint) if desc else dict(stride=stride, flen=flen, n=n)
-    if args.verify:  # trailers must be valid first
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr = torch.empty(n, dtype=torch.int32, device=dev) if header else None
+    if verify:  # trailers must be valid first
         vc.frames(flat, out_crc=crc, **kw)
         if desc:
             tidx = ((d_off + d_len.long())[:, None] + torch.arange(4, device=dev)[None, :]).reshape(-1)
             flat[tidx] = crc.view(torch.uint8)
         else:
             buf[:, flen:flen + 4] = crc.view(torch.uint8).view(n, 4)
+    bytes_per_launch = int(d_len.long().sum().item()) if desc else n * flen
+    # the whole job's CRC input per step: cfg4's one file, else every rank's own batch
+    file_crc_input = (n_total - 1) * (8 + payload + (8 if explicit else 0)) + 8 + (CFG4_FILE - (n_total - 1) * payload) \
+        + (8 if explicit else 0)
+    return dict(config=config, n=n, n_total=n_total, first=first, payload=payload, explicit=explicit, header=header,
+                strong=strong, ragged=ragged, desc=desc, buf=buf, flat=flat, flen=flen, stride=stride,
+                d_off=d_off, d_len=d_len, len_hint=len_hint, kw=kw, crc=crc, hdr=hdr,
+                bytes_per_launch=bytes_per_launch, job_bytes=file_crc_input if strong else None)
+
+
+def timed_steps(torch, dist, world, step, steps, warmup, stream):
+    """W untimed steps, then K steps bracketed by a barrier and a device
+    synchronise on both sides. Two HIP events bracket the K launches on
+    their stream: the launches run back to back as in a real window stream
+    (events between every step, as until round 3, put an event command
+    between the kernels: about 7 us per step, 0.3% of cfg3 and a fifth of
+    cfg2's 19 us launches). Returns (wall seconds, kernel ms per step = the
+    events' span over K, gaps between the launches included)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+
+def max_over_ranks(torch, dist, world, value, dev, backend):
+    t = torch.tensor([value], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def parity_sample(torch, w, rank, verify, nbad):
+    """This run's outputs against the oracle on a sample of frames (untimed)."""
+    from tests import _oracle
+
+    n, dev = w["n"], w["flat"].device
+    sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, min(n, 256), replace=False),
+                                           [0, n - 1]]))
+    if w["desc"]:
+        o = w["d_off"].cpu().numpy()[sample_idx]
+        l = w["d_len"].cpu().numpy()[sample_idx].astype(np.int64)
+        pieces = [w["flat"][int(a):int(a) + int(b)].cpu().numpy() for a, b in zip(o, l)]
+        rows = np.concatenate(pieces)
+        so = np.concatenate([[0], np.cumsum(l)[:-1]]).astype(np.uint64)
+        want = _oracle.frames(rows, so, l.astype(np.uint32))
+    else:
+        rows = w["buf"][torch.from_numpy(sample_idx).to(dev)].cpu().numpy().reshape(-1)
+        want = _oracle.frames_strided(rows, w["stride"], w["flen"], sample_idx.size)
+    got = w["crc"].cpu().numpy().view(np.uint32)[sample_idx] if not verify else want
+    ok = bool(np.array_equal(got, want))
+    if verify:
+        ok = ok and int(nbad.item()) == 0
+    return ok
+
+
+def rank_record(w, rank, gpu, steps, elapsed, kern_ms, parity):
+    b = w["bytes_per_launch"]
+    return {"rank": rank, "device": gpu, "frames": w["n"], "bytes_per_step": b,
+            "kernel_ms": round(kern_ms, 4), "elapsed_s": round(elapsed, 6),
+            "GiB_s": round(b * steps / elapsed / GIB, 2),
+            "kernel_GiB_s": round(b / (kern_ms * 1e-3) / GIB, 2), "parity_sample_ok": parity,
+            "last_frame_crc_input": int(w["d_len"][w["n"] - 1].item()) if w["desc"] and w["n"] else w["flen"]}
+
+
+def gather(dist, world, mine):
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def aggregate(per_rank, total_bytes, elapsed_max):
+    return {"total_bytes": total_bytes, "max_elapsed_s": round(elapsed_max, 6),
+            "slowest_rank": max(per_rank, key=lambda r: r["elapsed_s"])["rank"],
+            "sum_of_rank_GiB_s": round(sum(r["GiB_s"] for r in per_rank), 2)}
+
+
+def verify_windows(torch, vc, flat, dev, stream):
+    """VAL_RESUME_TAIL verify-window CRC: region windows
+    over the cfg5 stream, timed with HIP events on the launch stream. Each
+    size cycles over distinct windows spanning >= 1 GiB of the stream (or all
+    of it), more than the 256 MiB Infinity Cache, so no call re-reads bytes a
+    recent call left in a cache: the 8 MiB and 256 MiB rates are HBM rates.
+    Windows under 1 MiB are launch-bound; they take 128 windows spread over
+    the stream. The first and last window of each size are checked against
+    the oracle. Reported beside the frames number, never as `value`."""
+    from tests import _oracle
+
+    nb = int(flat.numel())
+    out = []
+    for wlen in (1 << 10, 8 << 10, 8 << 20, 256 << 20):
+        wlen = min(wlen, nb)
+        if wlen >= (1 << 20):
+            k = max(1, min(-(-(1 << 30) // wlen), nb // wlen))
+            starts = [j * wlen for j in range(k)]
+            span = k * wlen
+        else:
+            k = 128
+            gap = max(wlen, (nb - wlen) // k)
+            starts = [j * gap for j in range(k)]
+            span = k * wlen
+        reps = max(len(starts), 200 if wlen < (1 << 20) else 2 * len(starts))
+        st_out = torch.empty(1, dtype=torch.int32, device=dev)
+        vc.region(flat[starts[-1]:starts[-1] + wlen], out=st_out)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for r in range(reps):
+            o = starts[r % len(starts)]
+            vc.region(flat[o:o + wlen], out=st_out)
+        b.record(stream)
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / reps
+        ok = True
+        for o in (starts[0], starts[-1]):
+            vc.region(flat[o:o + wlen], out=st_out)
+            torch.cuda.synchronize()
+            ok = ok and ((int(st_out.item()) & 0xFFFFFFFF) ^ 0xFFFFFFFF) == _oracle.crc32(flat[o:o + wlen].cpu().numpy())
+        out.append({"bytes": wlen, "us": round(us, 2), "GiB_s": round(wlen / (us * 1e-6) / GIB, 1),
+                    "distinct_windows": len(starts), "bytes_cycled": span, "calls": reps, "crc_ok": ok})
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("VAL_BENCH_BACKEND", "nccl")
+    import torch
+    import torch.distributed as dist
+
+    ndev = torch.cuda.device_count()  # counts devices without initialising the GPU
+    if world > 1 and backend == "nccl" and ndev < world:
+        print(f"bench.py: WORLD_SIZE={world} ranks need {world} visible GPUs for the nccl (RCCL) backend, "
+              f"found {ndev}; one rank per GPU (VAL_BENCH_BACKEND=gloo rehearses several ranks on one GPU)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    gpu = local % max(ndev, 1)  # == local on a full node; with gloo a 1-GPU box rehearses N ranks
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{gpu}")
+    torch.cuda.set_device(dev)
+
+    import val_protocol_amd.crc as vc
+
+    vc.init(gpu)
+    w = build_workload(torch, dev, args.config, rank, world, args.verify, vc)
+    if w["ragged"] and args.sort_frames:
+        perm = torch.argsort(w["d_len"])
+        w["d_off"], w["d_len"] = w["d_off"][perm].contiguous(), w["d_len"][perm].contiguous()
+        w["kw"].update(off=w["d_off"], length=w["d_len"])
+    n, n_total, strong, ragged, header = w["n"], w["n_total"], w["strong"], w["ragged"], w["header"]
+    flat, buf, flen, stride, kw = w["flat"], w["buf"], w["flen"], w["stride"], w["kw"]
+    crc, hdr = w["crc"], w["hdr"]
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    pay = torch.empty(n, dtype=torch.int32, device=dev) if args.pay else None
+    nbad = torch.zeros(1, dtype=torch.int32, device=dev)
 
     # Batches smaller than the 256 MiB Infinity Cache (cfg2: 68 MB) would be
     # re-read from it by back-to-back steps. A real window stream hashes new
@@ -306,30 +487,8 @@ def main():
         else:
             vc.frames(src, out_crc=crc, out_hdr=hdr, **kw)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
-    # Two HIP events bracket the K launches on their stream: the launches run
-    # back to back as in a real window stream. (Events between every step, as
-    # until round 3, put an event command between the kernels: about 7 us per
-    # step, 0.3% of cfg3 and a fifth of cfg2's 19 us launches.) kernel_ms is
-    # the events' span over K, gaps between the launches included.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    elapsed, kern_ms = timed_steps(torch, dist, world, step, args.steps, args.warmup, stream)
     # per-step spread, from a short untimed pass with an event pair per step
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(min(args.steps, 5))]
     for a, b in evs:
@@ -338,46 +497,15 @@ def main():
         b.record(stream)
     torch.cuda.synchronize()
     print("[bench] per-step ms (untimed pass): " + " ".join(f"{a.elapsed_time(b):.4f}" for a, b in evs), file=sys.stderr)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    elapsed_max = max_over_ranks(torch, dist, world, elapsed, dev, backend)
     # algorithmic: CRC input of every frame (header_crc is a prefix: +0)
-    bytes_per_launch = int(d_len.long().sum().item()) if desc else n * flen
-
-    # Parity spot check of this run's output against the oracle (not timed).
-    sample_idx = np.unique(np.concatenate([np.random.default_rng(rank).choice(n, 256, replace=False), [0, n - 1]]))
-    from tests import _oracle
-
-    if desc:
-        o = d_off.cpu().numpy()[sample_idx]
-        l = d_len.cpu().numpy()[sample_idx].astype(np.int64)
-        pieces = [flat[int(a):int(a) + int(b)].cpu().numpy() for a, b in zip(o, l)]
-        rows = np.concatenate(pieces)
-        so = np.concatenate([[0], np.cumsum(l)[:-1]]).astype(np.uint64)
-        want = _oracle.frames(rows, so, l.astype(np.uint32))
-    else:
-        rows = buf[torch.from_numpy(sample_idx).to(dev)].cpu().numpy().reshape(-1)
-        want = _oracle.frames_strided(rows, stride, flen, sample_idx.size)
-    got = crc.cpu().numpy().view(np.uint32)[sample_idx] if not args.verify else want
-    parity = bool(np.array_equal(got, want))
-    if args.verify:
-        parity = parity and int(nbad.item()) == 0
+    bytes_per_launch = w["bytes_per_launch"]
+    parity = parity_sample(torch, w, rank, args.verify, nbad)
     # Per-rank record (BASELINE configs[3]: "per-GPU and aggregate GiB/s"):
     # each rank's own frames, kernel time by events and wall time between the
     # barriers; gathered on rank 0 (the only other collective of the run).
-    mine = {"rank": rank, "device": gpu, "frames": n, "bytes_per_step": bytes_per_launch,
-            "kernel_ms": round(kern_ms, 4), "elapsed_s": round(elapsed, 6),
-            "GiB_s": round(bytes_per_launch * args.steps / elapsed / GIB, 2),
-            "kernel_GiB_s": round(bytes_per_launch / (kern_ms * 1e-3) / GIB, 2), "parity_sample_ok": parity,
-            "last_frame_crc_input": int(d_len[n - 1].item()) if desc and n else flen}
-    per_rank = [mine]
-    if world > 1:
-        per_rank = [None] * world
-        dist.all_gather_object(per_rank, mine)
-
-    file_crc_input = (n_total - 1) * flen + 8 + (CFG4_FILE - (n_total - 1) * payload) + (8 if explicit else 0)
-    total_bytes = (file_crc_input if strong else bytes_per_launch * world) * args.steps
+    per_rank = gather(dist, world, rank_record(w, rank, gpu, args.steps, elapsed, kern_ms, parity))
+    total_bytes = (w["job_bytes"] if strong else bytes_per_launch * world) * args.steps
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
@@ -391,41 +519,16 @@ def main():
         hi = 2 * bytes_per_launch / (time.perf_counter() - t1) / GIB
         print(f"[bench] host-inclusive (pageable H2D + kernel + D2H): {hi:.2f} GiB/s", file=sys.stderr)
 
-    # cfg5 also names the VAL_RESUME_TAIL verify-window CRC:
-    # region windows over the same stream, timed with HIP events, each checked
-    # against the oracle. Reported beside the frames number, never as `value`.
-    windows = None
-    if ragged and rank == 0:
-        windows = []
-        for wlen in (1 << 10, 8 << 10, 8 << 20, 256 << 20):
-            wlen = min(wlen, int(flat.numel()))
-            win = flat[:wlen]
-            st_out = torch.empty(1, dtype=torch.int32, device=dev)
-            reps = 200 if wlen < (1 << 20) else 20
-            vc.region(win, out=st_out)
-            torch.cuda.synchronize()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            for _ in range(reps):
-                vc.region(win, out=st_out)
-            b.record(stream)
-            torch.cuda.synchronize()
-            us = a.elapsed_time(b) * 1e3 / reps
-            got = (int(st_out.item()) & 0xFFFFFFFF) ^ 0xFFFFFFFF
-            windows.append({"bytes": wlen, "us": round(us, 2), "GiB_s": round(wlen / (us * 1e-6) / GIB, 1),
-                            "crc_ok": got == _oracle.crc32(win.cpu().numpy())})
+    windows = verify_windows(torch, vc, flat, dev, stream) if ragged and rank == 0 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.sort_frames:
-        try:
-            avail = len(os.sched_getaffinity(0))
-        except AttributeError:
-            avail = os.cpu_count() or 1
-        threads = args.cpu_threads or min(16, avail)  # the GPU box's CPU share is 16 per GPU
-        all_threads = avail  # also N = all host cores visible to this process
+        visible, effective = effective_cpus()
+        threads = args.cpu_threads or min(16, effective)  # the GPU box's CPU share is 16 per GPU
+        all_threads = effective  # N = all host cores this process is granted
         if ragged:
-            offs_all = d_off.cpu().numpy()
-            lens_all = d_len.cpu().numpy().astype(np.uint32)
+            offs_all = w["d_off"].cpu().numpy()
+            lens_all = w["d_len"].cpu().numpy().astype(np.uint32)
             ends = offs_all + lens_all.astype(np.int64)
             ns = int(np.searchsorted(ends, 1 << 30, side="right"))  # ~1 GiB of the batch
             ns = max(1, min(ns, n))
@@ -442,10 +545,35 @@ def main():
         same = bool(np.array_equal(cout, crc[:ns].cpu().numpy().view(np.uint32))) if not args.verify else None
         cpu = {"value": round(cgibs, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
                "value_1core": round(one, 3), "value_all_cores": round(call, 3), "cores_all": all_threads,
-               "cpu_model": cpu_model(), "cores_visible": avail,
+               "cores_effective": effective, "cores_visible": visible, "cpu_model": cpu_model(),
                "sample": f"first {ns} frames of this batch ({sample_bytes / GIB:.2f} GiB of CRC input), "
                          f"reference val_crc32 per frame (src/val_core.c:150-160), frames round-robin over "
-                         f"pthreads, {detail}; outputs equal GPU: {same}"}
+                         f"pthreads, {detail}; all cores = the cgroup CPU quota ({effective} of {visible} "
+                         f"visible); outputs equal GPU: {same}"}
+
+    # BASELINE configs[3] in the same invocation: one 8 GiB file at MTU
+    # 65,536 sharded over the ranks by val_shard_frames (strong scaling),
+    # timed like the headline, its own per-rank records and aggregate.
+    strong_block = None
+    if not strong and not args.no_cfg4_strong and not args.verify and not args.sort_frames:
+        del flats, flat, buf, w, crc, hdr, ok, pay, kw
+        torch.cuda.empty_cache()
+        w4 = build_workload(torch, dev, "cfg4", rank, world, False, vc)
+        step4 = lambda: vc.frames(w4["flat"], out_crc=w4["crc"], **w4["kw"])  # noqa: E731
+        el4, km4 = timed_steps(torch, dist, world, step4, args.steps, min(args.warmup, 5), stream)
+        el4_max = max_over_ranks(torch, dist, world, el4, dev, backend)
+        par4 = parity_sample(torch, w4, rank, False, None)
+        pr4 = gather(dist, world, rank_record(w4, rank, gpu, args.steps, el4, km4, par4))
+        tb4 = w4["job_bytes"] * args.steps
+        strong_block = {
+            "workload": f"cfg4: one {CFG4_FILE >> 30} GiB file as {w4['n_total']} DATA frames of "
+                        f"{CONFIGS['cfg4'][1]} B payload (last frame {CFG4_FILE - (w4['n_total'] - 1) * CONFIGS['cfg4'][1]} B), "
+                        f"sharded over {world} GPU{'s' if world > 1 else ''} by contiguous byte-balanced frame ranges "
+                        f"(val_shard_frames, no collective), trailer CRC-32",
+            "scaling": "strong", "value": round(tb4 / el4_max / GIB, 2), "unit": "GiB/s",
+            "ms_per_step": round(el4_max / args.steps * 1e3, 4), "steps": args.steps,
+            "frames_total": w4["n_total"], "parity_sample_ok": all(r["parity_sample_ok"] for r in pr4),
+            "per_rank": pr4, "aggregate_over_max_rank": aggregate(pr4, tb4, el4_max)}
 
     if rank == 0:
         metric = "GiB/s device-resident trailer CRC-32 over batched DATA packets, 1 MI355X"
@@ -465,8 +593,9 @@ def main():
             "config": {
                 "workload": (f"{args.config}: {n_total if strong else n} DATA frames x "
                              + (f"{CFG5_MIN}-{CFG5_MAX} B log-uniform payload (1 in 8 implied offset), packed unaligned"
-                                if ragged else f"{payload} B payload"
-                                + (f" (last frame {CFG4_FILE - (n_total - 1) * payload} B: an 8 GiB file)" if strong else ""))
+                                if ragged else f"{w_payload(args.config)} B payload"
+                                + (f" (last frame {CFG4_FILE - (n_total - 1) * w_payload(args.config)} B: an 8 GiB file)"
+                                   if strong else ""))
                              + (f" (one file, sharded over {world} GPU{'s' if world > 1 else ''}), " if strong else " per GPU, ")
                              + f"{'header_crc + ' if header else ''}trailer CRC-32"
                              f"{' (RX verify)' if args.verify else ''}"
@@ -475,7 +604,7 @@ def main():
                 **({"frames_total": n_total} if strong else {}),
                 "crc_input_bytes_per_frame": (bytes_per_launch / n) if ragged else flen,
                 "frame_stride": stride if not ragged else "packed",
-                "lanes_per_frame": "per length class (2/4/8/16)" if ragged else vc.lanes_per_frame(len_hint),
+                "lanes_per_frame": "per length class (2/4/8/16)" if ragged else vc.lanes_per_frame(flen),
                 "parallelism": (f"one {n_total}-frame file sharded x{world} by contiguous frame ranges (no collective)"
                                 if strong else f"frame-sharded x{world} (no collective)"),
                 "parity_sample_ok": parity,
@@ -504,15 +633,17 @@ def main():
             "cpu_baseline": cpu,
             # per-GPU rates and the aggregate's denominator (BASELINE configs[3])
             "per_rank": per_rank,
-            "aggregate_over_max_rank": {
-                "total_bytes": total_bytes, "max_elapsed_s": round(elapsed_max, 6),
-                "slowest_rank": max(per_rank, key=lambda r: r["elapsed_s"])["rank"],
-                "sum_of_rank_GiB_s": round(sum(r["GiB_s"] for r in per_rank), 2)},
+            "aggregate_over_max_rank": aggregate(per_rank, total_bytes, elapsed_max),
+            **({"cfg4_strong": strong_block} if strong_block is not None else {}),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def w_payload(config):
+    return CONFIGS[config][1]
 
 
 if __name__ == "__main__":

@@ -15,6 +15,12 @@
 //   stream     plain read of the whole buffer, 4 KiB per wave per round
 //   +desc, +st, +sh  the frames pattern with the product's per-frame work
 //              added step by step (descriptors, output store, shuffles)
+//   rtL        (round 4) the frame length from a kernel argument: "frames"
+//              with the constant length had hipcc unroll the five rounds and
+//              issue them all at the group start; rtL keeps one round in
+//              flight, as the product does
+//   ilv16      (round 4) the frames pattern read as a 16-B interleave:
+//              instruction q covers G x 16 contiguous bytes of each frame
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -46,6 +52,11 @@ __device__ __forceinline__ void ld64(u32x4u (&v)[4], gu8 *p)
 #pragma unroll
     for (int q = 0; q < 4; q++) v[q] = *(gu32x4u *)(p + 16 * q);
 }
+__device__ __forceinline__ void ld64i(u32x4u (&v)[4], gu8 *p)  // 16-B interleave: instruction q at +16 G q
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = *(gu32x4u *)(p + 16 * kG * q);
+}
 __device__ __forceinline__ uint32_t xr(const u32x4u (&v)[4])
 {
     uint32_t a = 0;
@@ -57,7 +68,7 @@ __device__ __forceinline__ uint32_t xr(const u32x4u (&v)[4])
 // MODE 0 frames, 1 contig64, 2 contig16, 3 stream
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t bytes, uint32_t *out, const uint64_t *doff,
-                                              const uint32_t *dlen, uint32_t *outf)
+                                              const uint32_t *dlen, uint32_t *outf, uint32_t rtL)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * 1024 + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * 1024) >> 6;
@@ -76,7 +87,11 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
         // offsets from descriptor arrays (R and the unit grid per lane at run
         // time), 16 = one 4-B output store per frame, 32 = the wave-wide
         // min-reduction of round 0's first word and a log2(G) shuffle merge
-        constexpr bool DESC = MODE & 8, ST = MODE & 16, SH = MODE & 32;
+        // 64 = the length from a kernel argument (run-time geometry, as the
+        // product: no unrolled, hoisted rounds); 128 = the 16-B interleave
+        // (round span read as four instructions of G x 16 contiguous bytes
+        // per frame, lane g at 16 g; mb14)
+        constexpr bool DESC = MODE & 8, ST = MODE & 16, SH = MODE & 32, RTL = MODE & 64, ILV = MODE & 128;
         const int g = lane % kG;
         uint32_t nL = 0;  // DESC: the next group's descriptors, fetched while this group is read (as k_frames does)
         uint64_t noff = 0;
@@ -87,7 +102,7 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
         }
         for (uint64_t grp = wave; grp < kGroups; grp += nw) {
             const uint64_t f = grp * kGPW + lane / kG;
-            uint32_t L = kL;
+            uint32_t L = RTL ? rtL : kL;
             uint64_t off = f * kStride;
             if (DESC) {
                 L = nL;
@@ -102,13 +117,20 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
             gu8 *fp = (gu8 *)base + off;
             const int u0 = (int)U - (int)(kG * R) + g;
             u32x4u w0[4], nx[4];
-            if (R > 0 && u0 >= 0) {
-                const uint32_t inl = (uint32_t)((uintptr_t)fp & 127u);
-                const uint32_t skip = (u0 == 0 && pad > inl) ? pad - inl : 0u;
-                ld64(w0, fp + (int64_t)u0 * 64 - pad + skip);
+            if (ILV) {  // round r's span starts at fp + 64 (U - G R + G r) - pad; lane g at 16 g + 16 G q
+                gu8 *sp = fp + (int64_t)((int)U - (int)(kG * R)) * 64 - pad + 16 * g;
+                if (R > 0) ld64i(w0, sp);
+                if (R > 1) ld64i(nx, sp + kG * 64);
+            } else {
+                if (R > 0 && u0 >= 0) {
+                    const uint32_t inl = (uint32_t)((uintptr_t)fp & 127u);
+                    const uint32_t skip = (u0 == 0 && pad > inl) ? pad - inl : 0u;
+                    ld64(w0, fp + (int64_t)u0 * 64 - pad + skip);
+                }
+                if (R > 1) ld64(nx, fp + (int64_t)(u0 + kG) * 64 - pad);
             }
-            gu8 *up = fp + (int64_t)(u0 + kG) * 64 - pad;
-            if (R > 1) ld64(nx, up);
+            gu8 *up = ILV ? fp + (int64_t)((int)U - (int)(kG * R) + kG) * 64 - pad + 16 * g
+                          : fp + (int64_t)(u0 + kG) * 64 - pad;
             uint32_t a = 0;
             if (SH) {
                 int first = (R == 0 || u0 < 0) ? 16 : (u0 == 0 ? (int)(pad >> 2) : 0);
@@ -116,12 +138,15 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
                 for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
                 a = (uint32_t)__builtin_amdgcn_readfirstlane(first);
             }
-            if (R > 0 && u0 >= 0) a ^= xr(w0);
+            if (R > 0 && (ILV || u0 >= 0)) a ^= xr(w0);
             for (uint32_t r = 1; r < R; r++) {
                 u32x4u cur[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) cur[q] = nx[q];
-                if (r + 1 < R) ld64(nx, up + (uint64_t)r * kG * 64);
+                if (r + 1 < R) {
+                    if (ILV) ld64i(nx, up + (uint64_t)r * kG * 64);
+                    else ld64(nx, up + (uint64_t)r * kG * 64);
+                }
                 a = (a << 1 | a >> 31) ^ xr(cur);
             }
             if (SH) {
@@ -203,12 +228,17 @@ int main()
     const double crc_bytes = (double)kN * kL;
 #define RUN(M, name)                                                                                                 \
     {                                                                                                                \
-        const float ms = timeit([&] { hipLaunchKernelGGL((k_pat<M>), dim3(cus), dim3(1024), 0, 0, d, bytes, out, doff, dlen, outf); }); \
+        const float ms = timeit([&] { hipLaunchKernelGGL((k_pat<M>), dim3(cus), dim3(1024), 0, 0, d, bytes, out, doff, dlen, outf, kL); }); \
         printf("%-9s %.4f ms  %7.1f GB/s of CRC input (%llu x %u B)  %7.1f GB/s of buffer\n", name, ms,                \
                crc_bytes / ms / 1e6, (unsigned long long)kN, kL, (double)bytes / ms / 1e6);                            \
         fflush(stdout);                                                                                              \
     }
     for (int rep = 0; rep < 2; rep++) {
+        RUN(64, "frames rtL")
+        RUN(64 + 128, "ilv16 rtL")
+        RUN(64 + 16, "frames rtL st")
+        RUN(64 + 128 + 16, "ilv16 rtL st")
+        RUN(128, "ilv16")
         RUN(0, "frames")
         RUN(8, "+desc")
         RUN(24, "+desc+st")

@@ -158,7 +158,8 @@ val_status_t val_crc32_region_dev(const uint8_t *d_ptr, uint64_t len, uint32_t s
 /* Scratch bytes the region call needs for a given length (informational). */
 uint64_t val_crc32_region_scratch_bytes(uint64_t len);
 
-/* ---- batch frames, host memory (synchronous; H2D + kernel + D2H) --------
+/* ---- batch frames, host memory (synchronous; H2D + kernel + D2H, or the
+ * CPU engine below val_gpu_host_batch_min_bytes) ---------------------------
  * base_len bounds every frame: off[i] + len[i] (+4 for verify) <= base_len,
  * else VAL_ERR_INVALID_ARG. off/len NULL = strided mode as above.
  * Frames travel H2D in chunks of whole frames on a copy stream while the
@@ -172,6 +173,21 @@ val_status_t val_crc32_frames_host(const uint8_t *base, uint64_t base_len, const
 val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
                                           const uint32_t *len, uint64_t stride, uint32_t flen, uint32_t n, uint8_t *ok,
                                           uint32_t *nbad);
+
+/* Host batches whose CRC input totals fewer bytes than this are answered by
+ * this library's CPU engine instead of the GPU, with identical outputs: a
+ * host batch on the GPU pays a launch, a completion wait and PCIe for every
+ * byte, and below the measured crossover one CPU core
+ * is faster. -1 = VAL_GPU_HOST_BATCH_MIN_BYTES from the environment (read
+ * once), else the built-in default; 0 = always the GPU. Such batches need no
+ * device and are counted by val_gpu_cpu_batch_count. */
+void val_gpu_set_host_batch_min_bytes(int64_t bytes);
+uint64_t val_gpu_host_batch_min_bytes(void);
+uint64_t val_gpu_cpu_batch_count(void);
+/* Threads the CPU engine uses for one such batch: the calling thread plus
+ * threads - 1 helpers over byte-balanced frame ranges, at most one thread
+ * per 4 MiB of CRC input (default 1). */
+void val_gpu_set_host_cpu_threads(uint32_t threads);
 
 /* Host-memory form of val_crc32_verify_frames_ex_dev (pay: n entries, nullable). */
 val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
@@ -260,6 +276,17 @@ val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
  * (0, 1, 2 or 4; -1 = automatic: 1 for multi-pass batches, deeper when a batch
  * fits in one pass of the grid). Speed only; results never change. */
 val_status_t val_gpu_set_prefetch(int depth);
+/* Mixed-length descriptor batches (len_hint 0) of at least this many frames
+ * are binned by length on the device; smaller ones run uniform. -1 restores
+ * VAL_GPU_RAGGED_MIN_FRAMES from the environment (read once), else 4096.
+ * Speed only; results never change (tests pin the binned path with 1). */
+void val_gpu_set_ragged_min_frames(int64_t frames);
+uint32_t val_gpu_ragged_min_frames(void);
+/* Streams of `device` that hold library scratch (region accumulator, ragged
+ * binning, dynamic-tail queue); *evictions (nullable) = entries dropped so
+ * far, least recently used first, once more than 64 streams held scratch.
+ * Introspection for tests. */
+uint32_t val_gpu_scratch_entries(int device, uint64_t *evictions);
 
 #ifdef __cplusplus
 }

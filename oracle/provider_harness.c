@@ -33,6 +33,9 @@
  *       writes tests/golden/dropin_vectors.json (see mode_fixtures): what the
  *       GPU drop-in tests check the product against on the GPU box, where no
  *       reference code exists.
+ *   provider_harness none sessions
+ *       writes tests/golden/session_vectors.json (see mode_sessions): windowed
+ *       and resumed reference sessions, every frame logged.
  *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
  *       full val_send_files / val_receive_files transfer over an in-memory
  *       duplex pipe (the reference test strategy), provider on
@@ -130,6 +133,7 @@ static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
 typedef struct {
     uint8_t *bytes;   /* the whole frame as sent */
     size_t len;
+    unsigned long epoch;  /* the end's transport.recv calls before this send (sessions mode) */
 } frame_rec_t;
 
 typedef struct {
@@ -138,6 +142,7 @@ typedef struct {
     unsigned long frames;
     frame_rec_t *log;  /* optional frame log (fixtures mode): one record per transport.send */
     size_t nlog, caplog;
+    unsigned long recvs;  /* transport.recv calls of this end: frames sent between two are one window fill */
 } end_t;
 
 static int tp_send(void *ctx, const void *data, size_t len)
@@ -154,6 +159,7 @@ static int tp_send(void *ctx, const void *data, size_t len)
         r->bytes = (uint8_t *)malloc(len ? len : 1);
         memcpy(r->bytes, data, len);
         r->len = len;
+        r->epoch = e->recvs;
     }
     return pipe_push(e->out, (const uint8_t *)data, len);
 }
@@ -161,6 +167,7 @@ static int tp_send(void *ctx, const void *data, size_t len)
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
 {
     end_t *e = (end_t *)ctx;
+    e->recvs++;
     if (pipe_pop(e->in, (uint8_t *)buffer, size, timeout_ms)) {
         if (got) *got = size;
     } else if (got) {
@@ -930,9 +937,159 @@ static int mode_fixtures(void)
     return 0;
 }
 
+/* ---- sessions: real reference sessions for the call-site fixtures ---------
+ * `provider_harness none sessions > tests/golden/session_vectors.json`.
+ * Full val_send_files / val_receive_files transfers (reference built-in CRC)
+ * whose every transport.send is logged as in F6, plus each frame's window
+ * epoch: the number of transport.recv calls its end had made before the send,
+ * so frames sent back to back without a receive are one window fill of the
+ * sender (src/val_sender.c:822-841; include_offset = next_to_send ==
+ * last_acked, :833, visible as flags bit 0 of each DATA frame).
+ *   windowed loopbacks: tx_flow.window_cap_packets = 64 on both ends
+ *       (negotiation src/val_core.c:1755,1810-1834), initial window 64, at
+ *       MTU 1,024 and 16,404;
+ *   resumed VAL_RESUME_TAIL transfers: the receiver's output file already
+ *       holds a prefix of the input, so the receiver sends its tail-window
+ *       CRC in RESUME_RESP (src/val_receiver.c:158-181), the sender computes
+ *       the same window over its file and sends a VERIFY request
+ *       (src/val_sender.c:205-252), and the receiver checks it
+ *       (src/val_receiver.c:431-444): at the default 8 MiB cap, at 1 KiB,
+ *       and once with a byte of the receiver's tail flipped (verify fails).
+ * The wire is timing dependent (ACKs race the window fill), so this file is
+ * a recording, not a regenerable golden: tests check it for internal
+ * consistency on the CPU and replay it through the product on the GPU. */
+static void fx_log_epochs(const end_t *e, const uint8_t *file, size_t bytes)
+{
+    uint64_t next = 0;
+    for (size_t i = 0; i < e->nlog; i++) {
+        const uint8_t *f = e->log[i].bytes;
+        const size_t wl = e->log[i].len;
+        const uint32_t content = (uint32_t)f[2] | (uint32_t)f[3] << 8;
+        long long foff = -1;
+        size_t pre = wl - 4;
+        if (f[0] == VAL_PKT_DATA) {
+            const int explicit_off = f[1] & 1u;
+            const uint64_t off = explicit_off ? le64(f + 8) : next;
+            const uint32_t plen = content - (explicit_off ? 8u : 0u);
+            const uint8_t *pay = f + 8 + (explicit_off ? 8 : 0);
+            if (off + plen > bytes || memcmp(pay, file + off, plen) != 0) {
+                fprintf(stderr, "sessions: DATA frame %zu payload is not file[%llu:+%u]\n", i, (unsigned long long)off, plen);
+                exit(3);
+            }
+            foff = (long long)off;
+            next = off + plen;
+            pre = explicit_off ? 16 : 8;
+        }
+        printf("%s\n[%u,%zu,%u,%lld,", i ? "," : "", f[0], wl, le32(f + wl - 4), foff);
+        fx_hex(f, pre);
+        printf(",%lu]", e->log[i].epoch);
+    }
+}
+
+/* One session: `bytes` of input (oracle_prng_fill(seed)); when existing > 0
+ * the receiver's output file starts as the input's first `existing` bytes
+ * (byte `flip` XOR 0x5A when flip >= 0). */
+static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t window, uint32_t tail_cap, size_t existing,
+                      long long flip, uint64_t seed, int last)
+{
+    char tmpl[] = "/tmp/valssXXXXXX";
+    char *dir = mkdtemp(tmpl);
+    if (!dir) return 2;
+    char cwd[1024];
+    if (!getcwd(cwd, sizeof cwd) || chdir(dir) != 0) return 2;
+    const char *in = "input.bin", *outdir = "out", *out = "out/input.bin";
+    mkdir(outdir, 0777);
+    uint8_t *data = (uint8_t *)malloc(bytes);
+    oracle_prng_fill(seed, data, bytes);
+    FILE *f = fopen(in, "wb");
+    fwrite(data, 1, bytes, f);
+    fclose(f);
+    if (existing) {
+        uint8_t *part = (uint8_t *)malloc(existing);
+        memcpy(part, data, existing);
+        if (flip >= 0) part[flip] ^= 0x5A;
+        FILE *g = fopen(out, "wb");
+        fwrite(part, 1, existing, g);
+        fclose(g);
+        free(part);
+    }
+    pipe_t a2b, b2a;
+    pipe_init(&a2b, 64u << 20);
+    pipe_init(&b2a, 64u << 20);
+    end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0, NULL, 0, 0, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0, NULL, 0, 0, 0};
+    etx.caplog = erx.caplog = 4096;
+    etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
+    erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
+    val_config_t ctx_, crx;
+    make_cfg(&ctx_, &etx, mtu, NULL);
+    make_cfg(&crx, &erx, mtu, NULL);
+    ctx_.tx_flow.window_cap_packets = crx.tx_flow.window_cap_packets = window;
+    ctx_.tx_flow.initial_cwnd_packets = crx.tx_flow.initial_cwnd_packets = window;
+    ctx_.resume.tail_cap_bytes = crx.resume.tail_cap_bytes = tail_cap;
+    val_session_t *tx = NULL, *rx = NULL;
+    if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
+    rx_job_t job = {rx, outdir, VAL_OK};
+    pthread_t th;
+    pthread_create(&th, NULL, rx_main, &job);
+    const char *files[1] = {in};
+    val_status_t st = val_send_files(tx, files, 1, NULL);
+    pthread_join(th, NULL);
+    val_metrics_t mt, mr;
+    memset(&mt, 0, sizeof mt);
+    memset(&mr, 0, sizeof mr);
+    val_get_metrics(tx, &mt);
+    val_get_metrics(rx, &mr);
+    int equal = 0;
+    FILE *g = fopen(out, "rb");
+    if (g) {
+        uint8_t *back = (uint8_t *)malloc(bytes + 1);
+        size_t r = fread(back, 1, bytes + 1, g);
+        fclose(g);
+        equal = (r == bytes) && memcmp(back, data, bytes) == 0;
+        free(back);
+    }
+    printf("{\"name\":\"%s\",\"bytes\":%zu,\"mtu\":%zu,\"window_cap_packets\":%u,\"tail_cap_bytes\":%u,\"existing\":%zu,"
+           "\"flip\":%lld,\"file_seed\":%llu,\"tx_status\":%d,\"rx_status\":%d,\"equal\":%d,\"tx_crc_errors\":%u,"
+           "\"rx_crc_errors\":%u,\"retransmits\":%u,\"file_crc\":%u,\"tx_frames\":[",
+           name, bytes, mtu, window, tail_cap, existing, flip, (unsigned long long)seed, st, job.st, equal, mt.crc_errors,
+           mr.crc_errors, mt.retransmits + mr.retransmits, val_crc32(data, bytes));
+    fx_log_epochs(&etx, data, bytes);
+    printf("],\"rx_frames\":[");
+    fx_log_epochs(&erx, data, bytes);
+    printf("]}%s\n", last ? "" : ",");
+    val_session_destroy(tx);
+    val_session_destroy(rx);
+    for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
+    for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
+    free(etx.log);
+    free(erx.log);
+    free(data);
+    remove(out);
+    remove(in);
+    rmdir(outdir);
+    if (chdir(cwd) != 0) return 5;
+    rmdir(dir);
+    return 0;
+}
+
+static int mode_sessions(void)
+{
+    int rc = 0;
+    printf("{\"generator\":\"oracle/provider_harness none sessions (reference src/ built by oracle/Makefile, built-in CRC)\",\n"
+           "\"sessions\":[\n");
+    rc |= fx_session("window64_mtu1024", 600000, 1024, 64, 1024, 0, -1, 0x5E55101, 0);
+    rc |= fx_session("window64_mtu16404", 3u << 20, 16404, 64, 1024, 0, -1, 0x5E55102, 0);
+    rc |= fx_session("resume_tail_cap8m", (12u << 20) + 777u, 4096, 16, 0, (10u << 20) + 12345u, -1, 0x5E55103, 0);
+    rc |= fx_session("resume_tail_cap1k", 400000, 1024, 8, 1024, 300005, -1, 0x5E55104, 0);
+    rc |= fx_session("resume_tail_mismatch", 400000, 1024, 8, 8192, 300005, 300005 - 100, 0x5E55105, 1);
+    printf("]}\n");
+    return rc;
+}
+
 int main(int argc, char **argv)
 {
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
+    if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions();
     if (argc < 3) {
         fprintf(stderr, "usage: %s <libval_crc_hip.so|none> tx|rx|loopback [bytes mtu]\n", argv[0]);
         return 1;

@@ -12,6 +12,9 @@ if ROOT not in sys.path:
 # every hook call a GPU test checks runs on the GPU (child processes inherit
 # it); tests of the CPU engine set it explicitly (val_gpu_set_provider_min_bytes).
 os.environ["VAL_GPU_PROVIDER_MIN_BYTES"] = "0"
+# Likewise host-memory batch calls below the host-batch crossover run on the
+# CPU engine by design; the GPU suite sends every one to the GPU.
+os.environ["VAL_GPU_HOST_BATCH_MIN_BYTES"] = "0"
 
 
 def pytest_configure(config):
@@ -41,7 +44,9 @@ def _gpu_results_came_from_the_gpu(request):
         return
     import val_protocol_amd.crc as vc
 
-    before = vc.cpu_fallback_count(), vc.cpu_small_count()
+    before = vc.cpu_fallback_count(), vc.cpu_small_count(), vc.cpu_batch_count()
     yield
+    vc.set_ragged_min_frames(-1)  # tests pin the binned path with vc.set_ragged_min_frames(1)
     assert vc.cpu_fallback_count() == before[0], "a scalar hook fell back to the CPU during a GPU test"
     assert vc.cpu_small_count() == before[1], "a scalar hook answered below the threshold during a GPU test"
+    assert vc.cpu_batch_count() == before[2], "a host batch was answered by the CPU engine during a GPU test"

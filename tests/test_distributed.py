@@ -15,6 +15,8 @@ import torch.multiprocessing as mp
 
 from val_protocol_amd.shard import fold_partials, shard_frames, shard_region
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def test_shard_frames_partition():
     for n, w in [(0, 2), (1, 2), (7, 3), (1048576, 8), (131113, 8)]:
@@ -107,3 +109,18 @@ def test_fold_payload_states_host():
     ok[150] = 0
     st, nf = vc.fold_payload_states(0x1234, states, lens, ok)
     assert nf == 150 and st == _oracle.update_state(0x1234, data[:offs[150]])
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py under the driver's torchrun with the nccl (RCCL) backend and
+    fewer visible GPUs than ranks: exits non-zero with a clear message before
+    any GPU call or rendezvous (no GPU in this container: 0 < 2)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
+    env.pop("VAL_BENCH_BACKEND", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stderr[-1000:])
+    assert "need 2 visible GPUs" in r.stderr and r.stdout == ""

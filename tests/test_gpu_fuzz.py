@@ -61,9 +61,9 @@ def test_fuzz_batches(vc, monkeypatch):
         vc.set_geometry(int(rng.choice([0, 0, 0, 1, 2, 4, 8, 16, 32, 64])), int(rng.choice([-1, -1, 0, 1, 2])))
         vc.set_host_chunk_bytes(int(rng.choice([0, 0, 1 << 16, 1 << 20])))
         if rng.random() < 0.5:
-            monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+            vc.set_ragged_min_frames(1)
         else:
-            monkeypatch.delenv("VAL_GPU_RAGGED_MIN_FRAMES", raising=False)
+            vc.set_ragged_min_frames(-1)
         # device memory
         d = torch.from_numpy(base).to(dev)
         do = torch.from_numpy(offs.view(np.int64)).to(dev)

@@ -55,6 +55,17 @@ def test_bench_two_ranks_weak_cfg2():
     assert agg["max_elapsed_s"] == max(r["elapsed_s"] for r in pr)
     assert agg["total_bytes"] == 2 * 2 * 65536 * (8 + 8 + 1024)  # 2 ranks x 2 steps
     assert abs(line["value"] - agg["total_bytes"] / agg["max_elapsed_s"] / 2**30) / line["value"] < 0.01
+    # BASELINE configs[3] timed in the same invocation: the 8 GiB file sharded over the ranks
+    st = line["cfg4_strong"]
+    assert st["scaling"] == "strong" and st["frames_total"] == 131113 and st["parity_sample_ok"] is True
+    spr = st["per_rank"]
+    assert [r["rank"] for r in spr] == [0, 1] and sum(r["frames"] for r in spr) == 131113
+    assert spr[0]["frames"] in (65556, 65557)
+    # the file's 800-B remainder lands on the last rank
+    assert spr[-1]["last_frame_crc_input"] == 8 + 8 + 800 and spr[0]["last_frame_crc_input"] == 8 + 8 + 65516
+    file_crc_input = 131112 * (8 + 8 + 65516) + 8 + 8 + 800
+    assert st["aggregate_over_max_rank"]["total_bytes"] == 2 * file_crc_input  # 2 steps
+    assert st["value"] > 0
 
 
 def test_bench_two_ranks_strong_cfg4():

@@ -354,12 +354,12 @@ def test_host_pipeline_chunks(vc, pinned, chunk):
 
 
 def test_concurrent_streams_share_scratch(vc, dev, monkeypatch):
-    """Region and ragged calls on four streams at once: the context's scratch
-    arenas serialise them through events, every result bit-exact. The frame
+    """Region and ragged calls on four streams at once: each stream has its own
+    scratch (kept per stream handle), every result bit-exact. The frame
     batches take the device-binned path (its bucket totals are re-zeroed by
     each batch's last kernel for the next one) and differ in size, so the bin
     scratch also grows between calls."""
-    monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+    vc.set_ragged_min_frames(1)
     vc.set_geometry()
     streams = [torch.cuda.Stream() for _ in range(4)]
     regions, frames = [], []
@@ -442,9 +442,9 @@ def test_no_cpu_fallback_symbols_loaded(vc):
 
 # ---- ragged path: device binning by length class + grouped launch ------------
 @pytest.fixture
-def binned_always(monkeypatch):
+def binned_always(vc):
     """Pin the device-binned path even for batches below its size threshold."""
-    monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+    vc.set_ragged_min_frames(1)
 
 
 def _run_ragged(vc, dev, base, offs, lens, header=False):
@@ -463,7 +463,7 @@ def _run_ragged(vc, dev, base, offs, lens, header=False):
 @pytest.mark.parametrize("binned", [True, False])
 def test_ragged_binned(vc, dev, seed, n, lo, hi, binned, monkeypatch):
     if binned:
-        monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+        vc.set_ragged_min_frames(1)
     base, offs, lens = _ragged(seed, n, lo, hi)
     got, got_h = _run_ragged(vc, dev, base, offs, lens, header=True)
     want, want_h = _oracle.frames(base, offs, lens, header=True)
@@ -484,7 +484,7 @@ def test_ragged_log_uniform_cfg5_shape(vc, dev, binned_always):
 @pytest.mark.parametrize("binned", [True, False])
 def test_ragged_every_length_and_verify(vc, dev, binned, monkeypatch):
     if binned:
-        monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+        vc.set_ragged_min_frames(1)
     lens = np.arange(0, 2500, dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 4)]).astype(np.uint64)
     base = _prng.prng_bytes(57, int(offs[-1]) + 2600)
@@ -545,7 +545,7 @@ def test_wave_round_tail(vc, dev, L, extra):
     (False, 65516, 4),   # descriptor groups of 4 x 64 KiB: one queue word
     (True, 4184, 8),     # strided groups of 8 x 4.2 KiB (34 KB): 64 queue partitions
     (False, 4184, 8),    # descriptor groups of 8 x 4.2 KiB: 64 queue partitions
-    (False, 1084, 16),   # descriptor groups of 16 x 1.1 KiB (k_frames_carry): 64 queue partitions
+    (False, 1084, 16),   # descriptor groups of 16 x 1.1 KiB: 64 queue partitions, dequeued one group ahead
 ])
 def test_dynamic_tail_every_frame(vc, dev, strided, payload, per):
     """Launches long enough for the dynamic tail (k_frames: the last half of

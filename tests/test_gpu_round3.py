@@ -134,8 +134,8 @@ def test_short_dynamic_tail_every_frame(vc, dev):
 
 
 @pytest.fixture
-def binned_always(monkeypatch):
-    monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+def binned_always(vc):
+    vc.set_ragged_min_frames(1)
 
 
 @pytest.mark.parametrize("lo,hi", [(16400, 16400), (16385, 16896), (600, 600), (0, 0), (65000, 65536)])

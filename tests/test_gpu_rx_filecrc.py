@@ -55,7 +55,7 @@ def test_payload_states_device(vc, hint, seed, n, lo, hi, monkeypatch):
     import val_protocol_amd.wire as w
 
     if hint == "ragged":
-        monkeypatch.setenv("VAL_GPU_RAGGED_MIN_FRAMES", "1")
+        vc.set_ragged_min_frames(1)
     stream, fo, cl, pay_len, inc, file = _stream(seed, n, lo, hi)
     assert np.array_equal(w.payload_lens(stream, fo, cl), pay_len)
     dev = torch.device("cuda:0")

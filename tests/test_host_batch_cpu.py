@@ -1,0 +1,132 @@
+"""Host-memory batches below the host-batch crossover are answered by the
+library's CPU engine (val_crc32_hip.hip cpu_frames):
+the same outputs as the kernels, pinned here to the reference-written
+fixtures without a GPU. The windows, TX frames, RX verdicts and the 1 MiB
+loopback frame log in tests/golden/dropin_vectors.json were produced by the
+reference's own protocol code (src/val_core.c:718-1073, src/val_sender.c:
+258-315,822-841; oracle/provider_harness.c fixtures); header_crc and the
+payload states are checked against the oracle. The GPU suite forces the
+threshold to 0, so tests/test_gpu_dropin.py replays the same fixtures on the
+GPU path."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import val_protocol_amd.crc as vc
+import val_protocol_amd.wire as wire
+from tests import _oracle, _prng
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VAL_OK, VAL_ERR_CRC = 0, -6
+
+
+@pytest.fixture(scope="module")
+def fx():
+    with open(os.path.join(ROOT, "tests", "golden", "dropin_vectors.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(params=[1, 4], ids=["1thread", "4threads"])
+def cpu_routed(request):
+    """Every host batch below 2^62 bytes on the CPU engine, on 1 or 4 threads."""
+    vc.set_host_batch_min_bytes(1 << 62)
+    vc.set_host_cpu_threads(request.param)
+    before = vc.cpu_batch_count()
+    yield before
+    vc.set_host_batch_min_bytes(-1)
+    vc.set_host_cpu_threads(1)
+
+
+def _window(w):
+    file = _prng.prng_bytes(w["file_seed"], w["file_size"])
+    fr = np.array(w["frames"], dtype=np.uint64)
+    return wire.build_data_batch(file, fr[:, 0], fr[:, 1].astype(np.uint32), fr[:, 0], fr[:, 2].astype(np.uint8))
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_windows_match_reference(fx, cpu_routed, k):
+    w = fx["windows"][k]
+    stream, fo, cl = _window(w)
+    crc, hdr = vc.frames_host(stream, off=fo, length=cl, header=True)
+    assert crc.tolist() == w["trailers"]
+    assert np.array_equal(hdr, _oracle.frames(stream, fo, cl, header=True)[1])
+    wire.put_trailers(stream, fo, cl, crc)
+    assert _oracle.crc32(stream) == w["wire_crc"]
+    for _, pos, mask in w["corrupt"]:
+        stream[pos] ^= mask
+    st, fo2, cl2, consumed = wire.scan_frames(stream, w["mtu"])
+    assert st == VAL_OK and consumed == stream.size
+    vst, ok, nbad = vc.verify_frames_host(stream, off=fo2, length=cl2)
+    assert [bool(x) for x in ok] == [rc == VAL_OK for rc in w["ref_rc"]]
+    assert nbad == w["ref_crc_errors"] and vst == (VAL_ERR_CRC if nbad else VAL_OK)
+    assert vc.cpu_batch_count() - cpu_routed == 2
+
+
+def test_tx_frames_and_loopback_log(fx, cpu_routed):
+    frames, want = [], []
+    for r in fx["tx"]:
+        content = r["payload_len"] + (8 if r["include_offset"] else 0)
+        if content > 0xFFFF:
+            continue  # the reference's u16-wrapped frames (the product framer refuses them)
+        payload = _prng.prng_bytes(r["seed"], r["payload_len"])
+        stream, fo, cl = wire.build_data_batch(payload, [0], [payload.size], [r["offset"]], [r["include_offset"]])
+        frames.append(stream[:int(cl[0])])
+        want.append(r["trailer"])
+    off = np.concatenate([[0], np.cumsum([f.size + 4 for f in frames])[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(off[-1]) + frames[-1].size + 4, dtype=np.uint8)
+    for o, f in zip(off, frames):
+        buf[int(o):int(o) + f.size] = f
+    assert vc.frames_host(buf, off=off, length=np.array([f.size for f in frames], np.uint32)).tolist() == want
+    # BASELINE configs[0]: both sessions of the 1 MiB / MTU 1024 loopback
+    lb = fx["loopback"]
+    file = _prng.prng_bytes(lb["file_seed"], lb["bytes"])
+    for side in ("tx", "rx"):
+        parts, offs, lens, trailers, pos = [], [], [], [], 0
+        for ptype, wire_len, trailer, foff, prefix in lb[f"{side}_frames"]:
+            head = np.frombuffer(bytes.fromhex(prefix), dtype=np.uint8)
+            body = np.concatenate([head, file[foff:foff + wire_len - 4 - head.size]]) if ptype == 5 else head
+            parts += [body, np.frombuffer(int(trailer).to_bytes(4, "little"), dtype=np.uint8)]
+            offs.append(pos)
+            lens.append(body.size)
+            trailers.append(trailer)
+            pos += wire_len
+        stream = np.concatenate(parts)
+        offs, lens = np.array(offs, np.uint64), np.array(lens, np.uint32)
+        assert vc.frames_host(stream, off=offs, length=lens).tolist() == trailers
+        st, ok, nbad = vc.verify_frames_host(stream, off=offs, length=lens)
+        assert st == VAL_OK and nbad == 0 and ok.all()
+
+
+def test_strided_and_payload_states(cpu_routed):
+    """Strided batches and the RX payload-state by-product (f4) against the
+    oracle, including frames shorter than their prefix."""
+    n, flen, stride = 300, 1040, 1044
+    sb = _prng.prng_bytes(91, n * stride)
+    assert np.array_equal(vc.frames_host(sb, stride=stride, flen=flen, n=n), _oracle.frames_strided(sb, stride, flen, n))
+    rng = np.random.default_rng(92)
+    lens = rng.integers(0, 3000, 500).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 4)[:-1]]).astype(np.uint64)
+    base = _prng.prng_bytes(93, int(offs[-1]) + int(lens[-1]) + 4)
+    base[offs[::2].astype(np.int64) + 1] |= 1  # half the frames say "offset present" (16-B prefix)
+    base[offs[1::2].astype(np.int64) + 1] &= 0xFE
+    want = _oracle.frames(base, offs, lens)
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        base[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    base[int(offs[7]) + 2] ^= 0x10
+    st, ok, nbad, pay = vc.verify_frames_ex_host(base, off=offs, length=lens)
+    assert st == VAL_ERR_CRC and nbad == (1 if lens[7] > 2 else 0)
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        f = base[int(o):int(o) + int(L)]
+        pre = (16 if f[1] & 1 else 8) if L >= 8 else None
+        exp = _oracle.update_state(0, f[pre:]) if pre is not None and L >= pre else 0
+        assert int(pay[i]) == exp, i
+
+
+def test_threshold_knob():
+    vc.set_host_batch_min_bytes(12345)
+    assert vc.host_batch_min_bytes() == 12345
+    vc.set_host_batch_min_bytes(-1)
+    # the suite's conftest exports VAL_GPU_HOST_BATCH_MIN_BYTES=0 before the library loads
+    assert vc.host_batch_min_bytes() == int(os.environ.get("VAL_GPU_HOST_BATCH_MIN_BYTES", vc.host_batch_min_bytes()))

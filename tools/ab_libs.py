@@ -16,7 +16,7 @@ from tools.sweep_geometry import time_it  # noqa: E402
 
 def load(path):
     l = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
-    vc._declare(l)
+    vc._declare(l, strict=False)
     return l
 
 

@@ -12,11 +12,12 @@ in ``include/val_crc32_gpu.h``). Names mirror the reference interface:
   frames (reference ``src/val_core.c:828-834`` and ``:963-974``)
 * ``region`` -- long-window CRC (reference ``src/val_core.c:414-455``)
 
-Batch, region and device calls compute on the GPU; if the shared library is
-missing or the GPU path fails, calls raise (no CPU fallback). The scalar
-hooks answer inputs below the provider threshold with the library's own CPU
-engine by design (``provider_min_bytes``; 0 forces the GPU) and raise if
-the GPU path failed.
+Region and device calls compute on the GPU; if the shared library is
+missing or the GPU path fails, calls raise (no CPU fallback). By design, the
+scalar hooks answer inputs below the provider threshold, and the host-memory
+batch calls batches below the host-batch threshold, with the library's own
+CPU engine (``provider_min_bytes`` / ``host_batch_min_bytes``; 0 forces the
+GPU); above them a failed GPU path raises.
 """
 from __future__ import annotations
 
@@ -53,7 +54,9 @@ EXPORTS = (
     "val_frame_payload_lens", "val_gpu_set_provider_min_bytes", "val_gpu_provider_min_bytes",
     "val_gpu_cpu_small_count", "val_gpu_last_hook_path", "val_crc32_cpu_update_state", "val_crc32_cpu_engine",
     "val_crc32_fold_payload_states_at", "val_frame_data_offsets", "val_gpu_build_flags",
-    "val_gpu_host_copy_threads",
+    "val_gpu_host_copy_threads", "val_gpu_set_ragged_min_frames", "val_gpu_ragged_min_frames",
+    "val_gpu_scratch_entries", "val_gpu_set_host_batch_min_bytes", "val_gpu_host_batch_min_bytes",
+    "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads",
     "val_serialize_handshake", "val_deserialize_handshake", "val_serialize_meta", "val_deserialize_meta",
     "val_serialize_resume_resp", "val_deserialize_resume_resp", "val_serialize_verify_request",
     "val_deserialize_verify_request", "val_serialize_verify_response", "val_deserialize_verify_response",
@@ -78,8 +81,12 @@ _u64p = ctypes.POINTER(ctypes.c_uint64)
 _vp = ctypes.c_void_p
 
 
-def _declare(lib: ctypes.CDLL) -> None:
+def _declare(lib: ctypes.CDLL, strict: bool = True) -> None:
+    """Set argument and result types; strict=False skips symbols an older
+    build lacks (A/B tooling loads libraries of earlier revisions)."""
     def fn(name, res, *args):
+        if not strict and not hasattr(lib, name):
+            return
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = list(args)
@@ -139,6 +146,13 @@ def _declare(lib: ctypes.CDLL) -> None:
     fn("val_frame_data_offsets", None, _vp, _vp, _vp, u32, _vp)
     fn("val_gpu_build_flags", ctypes.c_char_p)
     fn("val_gpu_host_copy_threads", u32, u64, u32)
+    fn("val_gpu_set_ragged_min_frames", None, ctypes.c_int64)
+    fn("val_gpu_ragged_min_frames", u32)
+    fn("val_gpu_scratch_entries", u32, ctypes.c_int, ctypes.POINTER(u64))
+    fn("val_gpu_set_host_batch_min_bytes", None, ctypes.c_int64)
+    fn("val_gpu_host_batch_min_bytes", u64)
+    fn("val_gpu_cpu_batch_count", u64)
+    fn("val_gpu_set_host_cpu_threads", None, u32)
 
 
 def lib() -> ctypes.CDLL:
@@ -229,6 +243,44 @@ def set_provider_min_bytes(nbytes: int) -> None:
 
 def provider_min_bytes() -> int:
     return int(lib().val_gpu_provider_min_bytes())
+
+
+def set_host_batch_min_bytes(nbytes: int) -> None:
+    """Host batches with fewer CRC-input bytes than this are answered by the
+    CPU engine (0: always the GPU; -1: VAL_GPU_HOST_BATCH_MIN_BYTES or the
+    built-in crossover)."""
+    lib().val_gpu_set_host_batch_min_bytes(int(nbytes))
+
+
+def host_batch_min_bytes() -> int:
+    return int(lib().val_gpu_host_batch_min_bytes())
+
+
+def cpu_batch_count() -> int:
+    """Host batches answered by the CPU engine because they were below the threshold."""
+    return int(lib().val_gpu_cpu_batch_count())
+
+
+def set_host_cpu_threads(threads: int) -> None:
+    """Threads the CPU engine uses for one host batch below the threshold (default 1)."""
+    lib().val_gpu_set_host_cpu_threads(int(threads))
+
+
+def set_ragged_min_frames(frames: int) -> None:
+    """Mixed-length descriptor batches of at least `frames` frames take the
+    device-binned path (-1: VAL_GPU_RAGGED_MIN_FRAMES or the default 4096)."""
+    lib().val_gpu_set_ragged_min_frames(int(frames))
+
+
+def ragged_min_frames() -> int:
+    return int(lib().val_gpu_ragged_min_frames())
+
+
+def scratch_entries(device: int = 0) -> tuple[int, int]:
+    """(streams holding library scratch on `device`, LRU evictions so far)."""
+    ev = ctypes.c_uint64(0)
+    n = lib().val_gpu_scratch_entries(device, ctypes.byref(ev))
+    return int(n), int(ev.value)
 
 
 def cpu_update_state(state: int, data, engine: int = 0) -> int:

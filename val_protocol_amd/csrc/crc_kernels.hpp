@@ -197,6 +197,81 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp
     if (has) load_full(w, fp + ((int64_t)u * kUnit - pad) + (u == 0 ? unit0_line_skip(fp, pad) : 0u));
 }
 
+// 16-B interleaved loads of rounds >= 1 at G = 2 and 4 (round 4): a round's
+// G x 64-B span is read by four dwordx4 instructions, instruction q covering
+// the span's bytes [16 G q, 16 G (q + 1)) with lane g at 16 g, so one
+// instruction reads G x 16 contiguous bytes of each frame (the unit layout
+// reads 16 B at a 64-B lane stride: 32 B of each line per instruction). Lanes
+// then swap chunks inside their frame's lane group (DPP quad permutes: the G
+// lanes of a frame are one quad or one pair) so that each holds its own 64-B
+// unit again and the hash is unchanged. Lane g's register q holds span chunk
+// q G + g; unit g is chunks 4 g .. 4 g + 3. Same box against the unit
+// loads (profiles/r04_ab_ilv16.log): u1100d +2.7%, u600d +2.2%, u2000d
+// +2.1%, s1100 +0.8%; one-pass launches lost (cfg2 -3%), so the C0 kernels
+// keep the unit loads. -DVCRC_ILV16=0 builds the unit loads everywhere (A/B).
+#ifndef VCRC_ILV16
+#define VCRC_ILV16 1
+#endif
+template <int GT>
+constexpr bool ilv_lanes() { return VCRC_ILV16 && (GT == 2 || GT == 4); }
+
+__device__ __forceinline__ void load_ilv(uint32_t (&w)[kWords], gu8 *span_lane, int G)  // span_lane = span + 16 g
+{
+#pragma unroll
+    for (int q = 0; q < kWords / 4; q++) {
+        const u32x4u v = *reinterpret_cast<gu32x4u *>(span_lane + 16 * G * q);
+        w[4 * q + 0] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+    }
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int GT>
+__device__ __forceinline__ void ilv_to_units(uint32_t (&w)[kWords], int g)
+{
+    constexpr int kSwap1 = 0xB1, kSwap2 = 0x4E;  // quad_perm [1,0,3,2] and [2,3,0,1]
+    if (GT == 4) {
+        // 4 x 4 transpose of 16-B chunks in the quad: two butterfly stages
+        const bool o1 = g & 1, o2 = g & 2;
+#pragma unroll
+        for (int q = 0; q < 4; q += 2)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t r = quad_perm<kSwap1>(o1 ? w[4 * q + i] : w[4 * (q + 1) + i]);
+                if (o1) w[4 * q + i] = r;
+                else w[4 * (q + 1) + i] = r;
+            }
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t r = quad_perm<kSwap2>(o2 ? w[4 * q + i] : w[4 * (q + 2) + i]);
+                if (o2) w[4 * q + i] = r;
+                else w[4 * (q + 2) + i] = r;
+            }
+    } else if (GT == 2) {
+        // lane 0's unit = L0.R0 L1.R0 L0.R1 L1.R1; lane 1's = L0.R2 L1.R2 L0.R3 L1.R3
+        const bool o = g & 1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t a = quad_perm<kSwap1>(o ? w[i] : w[8 + i]);
+            const uint32_t b = quad_perm<kSwap1>(o ? w[4 + i] : w[12 + i]);
+            const uint32_t r0 = w[i], r1 = w[4 + i], r2 = w[8 + i], r3 = w[12 + i];
+            w[i] = o ? a : r0;
+            w[4 + i] = o ? r2 : a;
+            w[8 + i] = o ? b : r1;
+            w[12 + i] = o ? r3 : b;
+        }
+    }
+}
+
 // Mask and seed of unit-0 word i (frame offset q = 4i - pad): bytes before the
 // frame are zero and the seed is XORed into frame bytes 0..3.
 __device__ __forceinline__ uint32_t unit0_word(uint32_t x, int q, uint32_t seed)
@@ -319,11 +394,18 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
         h0 = ld32(hp);
         h1 = ld32(hp + 4);
     }
+    constexpr bool ILV = ilv_lanes<GT>() && !BF && !C0;
+    gu8 *const ilv_up = up - 48 * g;  // round 1's span + 16 g (ILV)
     uint32_t nxt[D][kWords];
     if (PF > 0) {
 #pragma unroll
-        for (int d = 0; d < D; d++)
-            if (BF || R > 1u + d) load_full(nxt[d], R > 1u + d ? up + d * kStep : dummy);
+        for (int d = 0; d < D; d++) {
+            if (ILV) {
+                if (R > 1u + d) load_ilv(nxt[d], ilv_up + d * kStep, G);
+            } else if (BF || R > 1u + d) {
+                load_full(nxt[d], R > 1u + d ? up + d * kStep : dummy);
+            }
+        }
     }
     uint32_t acc = 0;
     // Round 0's leading zero words (unit 0's front padding, lanes without a
@@ -362,7 +444,12 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     if (PF == 0) {
         for (uint32_t k = 1; k < R; k++, up += kStep) {
             uint32_t w[kWords];
-            load_full(w, up);
+            if (ILV) {
+                load_ilv(w, up - 48 * g, G);
+                ilv_to_units<GT>(w, g);
+            } else {
+                load_full(w, up);
+            }
             if (k == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
             if (G > 1) acc = map_apply(acc, gmap);
 #pragma unroll
@@ -378,7 +465,11 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
                     uint32_t w[kWords];
 #pragma unroll
                     for (int i = 0; i < kWords; i++) w[i] = nxt[d][i];
-                    if (kk + D < R) load_full(nxt[d], up + (uint64_t)(kk + D - 1) * kStep);
+                    if (kk + D < R) {
+                        if (ILV) load_ilv(nxt[d], ilv_up + (uint64_t)(kk + D - 1) * kStep, G);
+                        else load_full(nxt[d], up + (uint64_t)(kk + D - 1) * kStep);
+                    }
+                    if (ILV) ilv_to_units<GT>(w, g);
                     if (kk == 1 && seed_spill) w[0] ^= seed >> (8 * (kUnit - pad));
                     if (G > 1) acc = map_apply(acc, gmap);
 #pragma unroll

@@ -2,6 +2,7 @@
 // on MI355X (gfx950). Kernels: crc_kernels.hpp; device building blocks:
 // crc_device.hpp; algorithm and roofline: DESIGN.md; reference call sites per
 // entry point: include/val_crc32_gpu.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <sched.h>
@@ -34,9 +35,12 @@ namespace vcrc {
 // scratch kept per stream needs no events (an event record + wait per call
 // cost ~2.8 us of GPU time on 1 MiB windows, tools/ab_region.py). A stream is
 // keyed by its handle, and hipStreamPerThread (one handle naming a different
-// real stream on every host thread) by handle and thread. A destroyed
-// stream's handle is only reused once its work is done, so inheriting its
-// scratch is safe. Callers hold Ctx::mu from acquire through launch.
+// real stream on every host thread) by handle and a per-thread serial number
+// that is never reused (a std::thread::id is reused once its thread exits,
+// and the new thread would then share the old per-thread stream's scratch
+// while that stream's kernels may still run). A destroyed stream's handle is
+// only reused once its work is done, so inheriting its scratch is safe.
+// Callers hold Ctx::mu from acquire through launch.
 struct Arena {
     uint8_t *d = nullptr;
     size_t cap = 0;
@@ -45,14 +49,32 @@ struct Arena {
 
 struct StreamScratch {
     hipStream_t stream;
-    std::thread::id owner;  // the calling thread for hipStreamPerThread, else none
+    uint64_t owner;     // hipStreamPerThread: the calling thread's serial; else 0
+    uint64_t last_use;  // LRU tick (Ctx::scratch_tick)
+    // Bound to the dispatch of the last kernel that used this scratch
+    // (hipExtLaunchKernelGGL's stop event: no extra queue packet), so
+    // eviction waits for exactly that kernel without naming the stream,
+    // whose handle may have been destroyed since (HIP calls on a destroyed
+    // handle crash) or, for hipStreamPerThread, names another thread's stream.
+    hipEvent_t done = nullptr;
+    // used by a launch while its stream was capturing a graph: the graph may
+    // replay at any time, so the scratch is never evicted
+    bool captured = false;
     Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin;     // ragged binning: counts, plan, sorted order
     Arena queue;   // k_frames dynamic tail {head, exits} (zero between calls)
 };
-// Streams with scratch per device before the list is drained and dropped (a
-// program that keeps creating streams would otherwise grow it without bound).
+// Streams with scratch per device; beyond this the least recently used entry
+// is evicted (a program that keeps creating streams would otherwise grow the
+// list without bound).
 constexpr size_t kMaxStreamScratch = 64;
+std::atomic<uint64_t> g_thread_serial{0};
+thread_local uint64_t t_thread_serial = 0;  // 0: not assigned yet
+uint64_t thread_serial()
+{
+    if (!t_thread_serial) t_thread_serial = g_thread_serial.fetch_add(1) + 1;
+    return t_thread_serial;
+}
 
 // One context per HIP device: streams, constant blob, staging and scratch.
 // A process may drive any number of devices; each host thread works on the
@@ -62,6 +84,8 @@ constexpr size_t kMaxStreamScratch = 64;
 struct Ctx {
     std::recursive_mutex mu;
     std::vector<StreamScratch *> scratch;  // per stream handle
+    uint64_t scratch_tick = 0;
+    uint64_t scratch_evictions = 0;
     int device = -1;
     int cus = 0;
     hipStream_t stream = nullptr;
@@ -294,28 +318,27 @@ int prefetch_depth()
     return forced >= 0 ? forced : 1;
 }
 
+StreamScratch &scratch_for(Ctx &c, hipStream_t s);
+template <typename K, typename... Args>
+hipError_t launch_tracked(StreamScratch *x, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args);
+
 // one_pass: every wave hashes at most one frame group (windows, cfg2): round
 // 0's units by dword loads (k_frames C0; crc_kernels.hpp load_unit0).
+// x: the stream scratch the launch uses (the dynamic-tail queue), else null.
 template <int G>
-void launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p, bool one_pass)
+hipError_t launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p, bool one_pass, StreamScratch *x)
 {
-    if (p.out_pay) {  // payload states: the default depth only
-        hipLaunchKernelGGL((k_frames<G, 1, true>), grid, dim3(kBlock), 0, s, p);
-        return;
-    }
-    if (pf == 1 && one_pass) {
-        hipLaunchKernelGGL((k_frames<G, 1, false, true>), grid, dim3(kBlock), 0, s, p);
-        return;
-    }
+    const dim3 b(kBlock);
+    if (p.out_pay) return launch_tracked(x, k_frames<G, 1, true>, grid, b, s, p);  // payload states: default depth only
+    if (pf == 1 && one_pass) return launch_tracked(x, k_frames<G, 1, false, true>, grid, b, s, p);
     switch (pf) {
-    case 0: hipLaunchKernelGGL((k_frames<G, 0, false>), grid, dim3(kBlock), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((k_frames<G, 2, false>), grid, dim3(kBlock), 0, s, p); break;
-    case 4: hipLaunchKernelGGL((k_frames<G, 4, false>), grid, dim3(kBlock), 0, s, p); break;
-    default: hipLaunchKernelGGL((k_frames<G, 1, false>), grid, dim3(kBlock), 0, s, p); break;
+    case 0: return launch_tracked(x, k_frames<G, 0, false>, grid, b, s, p);
+    case 2: return launch_tracked(x, k_frames<G, 2, false>, grid, b, s, p);
+    case 4: return launch_tracked(x, k_frames<G, 4, false>, grid, b, s, p);
+    default: return launch_tracked(x, k_frames<G, 1, false>, grid, b, s, p);
     }
 }
 
-StreamScratch &scratch_for(Ctx &c, hipStream_t s);
 val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out);
 
 // Dynamic tail of long uniform launches (k_frames): VAL_GPU_DYNAMIC_TAIL=0/1.
@@ -412,8 +435,10 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     // unless the lock is held until the kernel is launched
     Ctx &cm = const_cast<Ctx &>(c);
     std::lock_guard<std::recursive_mutex> lk(cm.mu);
+    StreamScratch *used = nullptr;
     if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
-        Arena &a = scratch_for(cm, s).queue;
+        used = &scratch_for(cm, s);
+        Arena &a = used->queue;
         uint8_t *q = nullptr;
         val_status_t st = arena_acquire(a, kDynQueueBytes, s, &q);
         if (st != VAL_OK) return st;
@@ -427,17 +452,18 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
         p.static_rounds = (uint32_t)(VCRC_DYN_DIV == 1 ? 1u : rounds - std::max<uint64_t>(1, rounds / VCRC_DYN_DIV));
     }
     const bool one_pass = ((uint64_t)p.n + 64 / G - 1) / (64 / G) <= (uint64_t)grid.x * kWavesPerBlock;
+    hipError_t e = hipSuccess;
     switch (G) {
-    case 1: launch_uniform_g<1>(pf, grid, s, p, one_pass); break;
-    case 2: launch_uniform_g<2>(pf, grid, s, p, one_pass); break;
-    case 4: launch_uniform_g<4>(pf, grid, s, p, one_pass); break;
-    case 8: launch_uniform_g<8>(pf, grid, s, p, one_pass); break;
-    case 16: launch_uniform_g<16>(pf, grid, s, p, one_pass); break;
-    case 32: launch_uniform_g<32>(pf, grid, s, p, one_pass); break;
-    case 64: launch_uniform_g<64>(pf, grid, s, p, one_pass); break;
+    case 1: e = launch_uniform_g<1>(pf, grid, s, p, one_pass, used); break;
+    case 2: e = launch_uniform_g<2>(pf, grid, s, p, one_pass, used); break;
+    case 4: e = launch_uniform_g<4>(pf, grid, s, p, one_pass, used); break;
+    case 8: e = launch_uniform_g<8>(pf, grid, s, p, one_pass, used); break;
+    case 16: e = launch_uniform_g<16>(pf, grid, s, p, one_pass, used); break;
+    case 32: e = launch_uniform_g<32>(pf, grid, s, p, one_pass, used); break;
+    case 64: e = launch_uniform_g<64>(pf, grid, s, p, one_pass, used); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
-    VCRC_HIP(hipGetLastError(), "k_frames launch");
+    VCRC_HIP(e, "k_frames launch");
     return VAL_OK;
 }
 
@@ -482,25 +508,82 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t l
 
 void arena_free(Arena &a);
 
+void scratch_free(StreamScratch *x)
+{
+    arena_free(x->region);
+    arena_free(x->queue);
+    arena_free(x->bin);
+    if (x->done) (void)hipEventDestroy(x->done);
+    delete x;
+}
+
+// Wait until no kernel still uses x's scratch: its last kernel's completion
+// event. False when the entry cannot be drained (graph capture) or the wait
+// failed; the caller then evicts another entry.
+bool scratch_drain(StreamScratch *x)
+{
+    if (x->captured || !x->done) return false;
+    if (hipEventSynchronize(x->done) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
+// Scratch of stream s (the calling thread's per-thread stream for
+// hipStreamPerThread). A full list evicts its least recently used entry
+// after draining it (scratch_drain); if no entry can be drained (every other
+// one is captured in a graph), the list grows past its cap.
 StreamScratch &scratch_for(Ctx &c, hipStream_t s)
 {
-    const std::thread::id who = s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+    const uint64_t who = s == hipStreamPerThread ? thread_serial() : 0u;
+    const uint64_t tick = ++c.scratch_tick;
     for (StreamScratch *x : c.scratch)
-        if (x->stream == s && x->owner == who) return *x;
-    if (c.scratch.size() >= kMaxStreamScratch) {
-        // every stream drained, so no kernel still uses any of these blocks
-        (void)hipDeviceSynchronize();
-        for (StreamScratch *x : c.scratch) {
-            arena_free(x->region);
-            arena_free(x->queue);
-            arena_free(x->bin);
-            delete x;
+        if (x->stream == s && x->owner == who) {
+            x->last_use = tick;
+            return *x;
         }
-        c.scratch.clear();
+    if (c.scratch.size() >= kMaxStreamScratch) {
+        std::vector<StreamScratch *> by_age(c.scratch);
+        std::sort(by_age.begin(), by_age.end(),
+                  [](const StreamScratch *a, const StreamScratch *b) { return a->last_use < b->last_use; });
+        for (StreamScratch *x : by_age) {
+            if (!scratch_drain(x)) continue;
+            c.scratch.erase(std::find(c.scratch.begin(), c.scratch.end(), x));
+            scratch_free(x);
+            c.scratch_evictions++;
+            break;
+        }
     }
-    c.scratch.push_back(new StreamScratch{s, who, {}, {}, {}});
-    return *c.scratch.back();
+    StreamScratch *x = new StreamScratch{s, who, tick};
+    if (hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        x->done = nullptr;  // never drained: never evicted
+    }
+    c.scratch.push_back(x);
+    return *x;
 }
+
+// Launch a kernel that uses x's scratch, binding x's completion event to the
+// dispatch. While s is capturing a graph the kernel is launched plainly and
+// the entry is kept for good (the graph owns that use of the scratch).
+template <typename K, typename... Args>
+hipError_t launch_tracked(StreamScratch *x, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args)
+{
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (x && hipStreamIsCapturing(s, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        cap = hipStreamCaptureStatusActive;  // unknown: treat as captured
+    }
+    if (x && cap == hipStreamCaptureStatusNone && x->done) {
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, nullptr, x->done, 0u, args...);
+    } else {
+        if (x) x->captured = true;
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+    }
+    return hipGetLastError();
+}
+
 
 // Scratch of at least `bytes` for stream s. Growing waits for the stream's
 // earlier kernels, which may still use the old block.
@@ -540,7 +623,8 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
     const size_t sz_heads = (size_t)kQueueParts * 64u, sz_gcount = (size_t)kBuckets * 4u;
     const size_t total = sz_heads + sz_gcount + 64u + (size_t)nbin * kBuckets * 4u + (size_t)n * 4u;
     std::lock_guard<std::recursive_mutex> lk(c.mu);
-    Arena &a = scratch_for(c, s).bin;
+    StreamScratch &ss = scratch_for(c, s);
+    Arena &a = ss.bin;
     uint8_t *scratch = nullptr;
     val_status_t st = arena_acquire(a, total, s, &scratch);
     if (st != VAL_OK) return st;
@@ -565,10 +649,10 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
         const uint64_t max_items = (n + 3u) / 4u + kClasses;  // every class packs >= 4 frames per item
         const unsigned blocks = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>((uint64_t)c.cus, (max_items + kWavesPerBlock - 1) / kWavesPerBlock));
-        if (p.out_pay) hipLaunchKernelGGL((k_frames_ragged<1, true>), dim3(blocks), dim3(kBlock), 0, s, p);
-        else if (forced_prefetch() == 0) hipLaunchKernelGGL((k_frames_ragged<0, false>), dim3(blocks), dim3(kBlock), 0, s, p);
-        else hipLaunchKernelGGL((k_frames_ragged<1, false>), dim3(blocks), dim3(kBlock), 0, s, p);
-        e = hipGetLastError();
+        // the ragged kernel is the last of the three on the stream to use the scratch
+        if (p.out_pay) e = launch_tracked(&ss, k_frames_ragged<1, true>, dim3(blocks), dim3(kBlock), s, p);
+        else if (forced_prefetch() == 0) e = launch_tracked(&ss, k_frames_ragged<0, false>, dim3(blocks), dim3(kBlock), s, p);
+        else e = launch_tracked(&ss, k_frames_ragged<1, false>, dim3(blocks), dim3(kBlock), s, p);
         a.counts_zero = e == hipSuccess;
     }
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
@@ -578,11 +662,32 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
 // typical_len == 0 with descriptors means "lengths unknown or mixed": bin them,
 // unless the batch is too small to fill the machine once (binning is four
 // launches; a small window runs uniform at 16 lanes per frame instead).
-// VAL_GPU_RAGGED_MIN_FRAMES overrides the threshold (tests pin the binned path on small batches).
+// val_gpu_set_ragged_min_frames, else VAL_GPU_RAGGED_MIN_FRAMES (read once),
+// overrides the threshold (tests pin the binned path on small batches).
+constexpr uint32_t kRaggedMinFrames = 4096;
+std::atomic<int64_t> g_ragged_min{-1};  // -1: from the environment, else the default
+
+// A size knob from the environment, read once: a malformed value (e.g. "1M")
+// is reported once on stderr and the built-in default is used.
+int64_t env_size(const char *name)
+{
+    const char *e = getenv(name);
+    if (!e || !*e) return -1;
+    char *end = nullptr;
+    const long long v = strtoll(e, &end, 0);
+    if (end == e || *end != '\0' || v < 0) {
+        fprintf(stderr, "val_crc32_gpu: ignoring %s=\"%s\" (not a non-negative integer); using the default\n", name, e);
+        return -1;
+    }
+    return (int64_t)v;
+}
+
 uint32_t ragged_min_frames()
 {
-    const char *e = getenv("VAL_GPU_RAGGED_MIN_FRAMES");
-    return e ? (uint32_t)atoi(e) : 4096u;
+    const int64_t v = g_ragged_min.load(std::memory_order_relaxed);
+    if (v >= 0) return (uint32_t)std::min<int64_t>(v, UINT32_MAX);
+    static const int64_t env = env_size("VAL_GPU_RAGGED_MIN_FRAMES");
+    return env >= 0 ? (uint32_t)std::min<int64_t>(env, UINT32_MAX) : kRaggedMinFrames;
 }
 
 val_status_t launch_frames(Ctx &c, FrameParams &p, uint32_t typical_len, hipStream_t s)
@@ -640,7 +745,8 @@ val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t sta
         return st;
     }
     std::lock_guard<std::recursive_mutex> lk(c.mu);
-    Arena &a = scratch_for(c, s).region;
+    StreamScratch &ss = scratch_for(c, s);
+    Arena &a = ss.region;
     uint8_t *scratch = nullptr;
     val_status_t st = arena_acquire(a, 128, s, &scratch);
     if (st != VAL_OK) return st;
@@ -657,8 +763,7 @@ val_status_t region_dev(Ctx &c, const uint8_t *d_ptr, uint64_t len, uint32_t sta
         rp.out = d_out;
         rp.acc = reinterpret_cast<uint32_t *>(scratch);
         rp.consts = c.d_consts;
-        hipLaunchKernelGGL(k_region, dim3(rp.nwg), dim3(kBlock), 0, s, rp);
-        e = hipGetLastError();
+        e = launch_tracked(&ss, k_region, dim3(rp.nwg), dim3(kBlock), s, rp);
         a.counts_zero = e == hipSuccess;  // the last workgroup re-zeroes the scratch
     }
     if (e != hipSuccess) return fail(VAL_ERR_IO, "k_region launch", e);
@@ -861,8 +966,7 @@ uint64_t provider_min_bytes()
 {
     const int64_t v = g_provider_min.load(std::memory_order_relaxed);
     if (v >= 0) return (uint64_t)v;
-    static const int64_t env = getenv("VAL_GPU_PROVIDER_MIN_BYTES") ? strtoll(getenv("VAL_GPU_PROVIDER_MIN_BYTES"), nullptr, 0)
-                                                                    : -1;
+    static const int64_t env = env_size("VAL_GPU_PROVIDER_MIN_BYTES");
     return env >= 0 ? (uint64_t)env : (uint64_t)VCRC_PROVIDER_MIN_BYTES;
 }
 
@@ -971,6 +1075,87 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
     return VAL_OK;
 }
 
+// ---- host-memory batches below the measured crossover: the CPU engine --------
+// A host batch on the GPU pays a launch, a completion wait and PCIe for every
+// byte (51 GiB/s at best), while one core of the CPU
+// engine folds 41-47 GB/s from DRAM: below the crossover (DESIGN.md section 1,
+// tools/host_crossover.py) the *_frames_host calls answer with the CPU engine
+// on the calling thread (val_gpu_set_host_cpu_threads adds helper threads),
+// with the same outputs as the kernels: trailer CRC, header_crc, verify flags
+// and count, payload states. Counted (val_gpu_cpu_batch_count);
+// VAL_GPU_HOST_BATCH_MIN_BYTES or val_gpu_set_host_batch_min_bytes moves the
+// threshold (0 = always the GPU: the GPU test suite sets it).
+#ifndef VCRC_HOST_BATCH_MIN_BYTES  // measured crossover at one CPU thread, DESIGN.md section 1
+#define VCRC_HOST_BATCH_MIN_BYTES (64u << 20)
+#endif
+std::atomic<int64_t> g_host_batch_min{-1};  // -1: from the environment, else the default
+std::atomic<uint32_t> g_host_cpu_threads{1};
+std::atomic<uint64_t> g_cpu_batches{0};
+
+uint64_t host_batch_min_bytes()
+{
+    const int64_t v = g_host_batch_min.load(std::memory_order_relaxed);
+    if (v >= 0) return (uint64_t)v;
+    static const int64_t env = env_size("VAL_GPU_HOST_BATCH_MIN_BYTES");
+    return env >= 0 ? (uint64_t)env : (uint64_t)VCRC_HOST_BATCH_MIN_BYTES;
+}
+
+std::vector<uint32_t> shard_cuts(uint32_t n, const uint32_t *len, uint32_t world);
+
+// Frames [i0, i1) of a host batch on the CPU engine (outputs as frames_host).
+uint32_t cpu_frames_range(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                          uint32_t flen, uint32_t i0, uint32_t i1, int verify, uint32_t *crc, uint32_t *hdr,
+                          uint8_t *ok, uint32_t *pay)
+{
+    uint32_t bad = 0;
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint8_t *p = base + (off ? off[i] : (uint64_t)i * stride);
+        const uint32_t L = len ? len[i] : flen;
+        const uint32_t c = vcrc_cpu_update(0xFFFFFFFFu, p, L) ^ 0xFFFFFFFFu;
+        if (crc) crc[i] = c;
+        if (hdr) hdr[i] = vcrc_cpu_update(0xFFFFFFFFu, p, std::min<uint32_t>(L, 8u)) ^ 0xFFFFFFFFu;
+        if (pay) {
+            // the kernels' payload by-product: the register of the payload from
+            // zero, after the 8-B header and the 8-B offset when flags say so
+            const uint32_t pre = L >= 8 ? ((p[1] & VAL_DATA_OFFSET_PRESENT) ? 16u : 8u) : UINT32_MAX;
+            pay[i] = (L >= 8 && L >= pre) ? vcrc_cpu_update(0u, p + pre, L - pre) : 0u;
+        }
+        if (verify) {
+            const uint32_t t = (uint32_t)p[L] | (uint32_t)p[L + 1] << 8 | (uint32_t)p[L + 2] << 16 |
+                               (uint32_t)p[L + 3] << 24;
+            if (ok) ok[i] = c == t ? 1u : 0u;
+            bad += c != t;
+        }
+    }
+    return bad;
+}
+
+// The whole batch on the calling thread plus helper threads (contiguous
+// frame ranges balanced by bytes, as the multi-GPU split).
+// Helper threads only for batches of at least 4 MiB per thread: a thread
+// start costs more than a small window's whole CRC.
+uint32_t cpu_frames(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t flen,
+                    uint32_t n, uint64_t total, int verify, uint32_t *crc, uint32_t *hdr, uint8_t *ok, uint32_t *pay)
+{
+    g_cpu_batches.fetch_add(1, std::memory_order_relaxed);
+    const uint64_t by_size = std::max<uint64_t>(1, total >> 22);
+    const uint32_t nt = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>({(uint64_t)g_host_cpu_threads.load(), by_size, (uint64_t)std::max(n, 1u)}));
+    if (nt == 1) return cpu_frames_range(base, off, len, stride, flen, 0, n, verify, crc, hdr, ok, pay);
+    const std::vector<uint32_t> cut = shard_cuts(n, len, nt);
+    std::vector<uint32_t> bad(nt, 0);
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; t++)
+        th.emplace_back([&, t] {
+            bad[t] = cpu_frames_range(base, off, len, stride, flen, cut[t], cut[t + 1], verify, crc, hdr, ok, pay);
+        });
+    bad[0] = cpu_frames_range(base, off, len, stride, flen, cut[0], cut[1], verify, crc, hdr, ok, pay);
+    for (auto &x : th) x.join();
+    uint32_t nbad = 0;
+    for (uint32_t b : bad) nbad += b;
+    return nbad;
+}
+
 // Host-memory batches on the calling thread's device: descriptors H2D once,
 // then frames in chunks of whole frames (<= host_chunk_bytes of wire span
 // each) through two device slots: chunk c's H2D on the copy stream overlaps
@@ -985,6 +1170,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
     if ((off == nullptr) != (len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
     const uint64_t tail = verify ? 4u : 0u;
     uint32_t lmin = UINT32_MAX, lmax = 0;
+    uint64_t total = 0;
     bool monotone = true;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t o = off ? off[i] : (uint64_t)i * stride;
@@ -992,7 +1178,13 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         if (o > base_len || l + tail > base_len - o) return fail(VAL_ERR_INVALID_ARG, "frame overruns the buffer");
         lmin = std::min<uint32_t>(lmin, (uint32_t)l);
         lmax = std::max<uint32_t>(lmax, (uint32_t)l);
+        total += l;
         if (off && i && off[i] < off[i - 1]) monotone = false;
+    }
+    if (total < host_batch_min_bytes()) {  // below the crossover: the CPU engine (no device needed)
+        const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, pay);
+        if (nbad) *nbad = verify ? bad : 0u;
+        return VAL_OK;
     }
     DeviceScope ds;
     Ctx *cp = nullptr;
@@ -1320,12 +1512,7 @@ void ctx_free(Ctx &c)
         if (c.kern_done[k]) (void)hipEventDestroy(c.kern_done[k]);
     }
     (void)hipDeviceSynchronize();  // the streams that used the scratch may be gone
-    for (StreamScratch *x : c.scratch) {
-        arena_free(x->region);
-        arena_free(x->queue);
-        arena_free(x->bin);
-        delete x;
-    }
+    for (StreamScratch *x : c.scratch) scratch_free(x);
     c.scratch.clear();
     if (c.h_out) (void)hipHostFree(c.h_out);
     if (c.copy) (void)hipStreamDestroy(c.copy);
@@ -1457,6 +1644,32 @@ const char *val_gpu_build_flags(void)
 void val_gpu_set_provider_min_bytes(int64_t bytes) { g_provider_min.store(bytes < 0 ? -1 : bytes); }
 
 uint64_t val_gpu_provider_min_bytes(void) { return provider_min_bytes(); }
+
+void val_gpu_set_host_batch_min_bytes(int64_t bytes) { g_host_batch_min.store(bytes < 0 ? -1 : bytes); }
+
+uint64_t val_gpu_host_batch_min_bytes(void) { return host_batch_min_bytes(); }
+
+uint64_t val_gpu_cpu_batch_count(void) { return g_cpu_batches.load(std::memory_order_relaxed); }
+
+void val_gpu_set_host_cpu_threads(uint32_t threads)
+{
+    g_host_cpu_threads.store(std::max<uint32_t>(1, std::min<uint32_t>(threads, 256)));
+}
+
+void val_gpu_set_ragged_min_frames(int64_t frames) { g_ragged_min.store(frames < 0 ? -1 : frames); }
+
+uint32_t val_gpu_ragged_min_frames(void) { return ragged_min_frames(); }
+
+uint32_t val_gpu_scratch_entries(int device, uint64_t *evictions)
+{
+    if (evictions) *evictions = 0;
+    if (device < 0 || device >= kMaxDevices) return 0;
+    Ctx *c = g_ctxs[device].load(std::memory_order_acquire);
+    if (!c) return 0;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (evictions) *evictions = c->scratch_evictions;
+    return (uint32_t)c->scratch.size();
+}
 
 uint64_t val_gpu_cpu_small_count(void) { return g_cpu_small.load(std::memory_order_relaxed); }
 
