@@ -206,14 +206,19 @@ __device__ __forceinline__ void load_unit0(uint32_t (&w)[kWords], int u, gu8 *fp
 // lanes of a frame are one quad or one pair) so that each holds its own 64-B
 // unit again and the hash is unchanged. Lane g's register q holds span chunk
 // q G + g; unit g is chunks 4 g .. 4 g + 3. Same box against the unit
-// loads (profiles/r04_ab_ilv16.log): u1100d +2.7%, u600d +2.2%, u2000d
-// +2.1%, s1100 +0.8%; one-pass launches lost (cfg2 -3%), so the C0 kernels
-// keep the unit loads. -DVCRC_ILV16=0 builds the unit loads everywhere (A/B).
+// loads (profiles/r04_ab_ilv16.log, r04_ab_ilv16_ragged.log): u1100d
+// +1.7-2.7%, u600d +2.2%, u2000d +2.1%, s1100 0 to +0.8%; one-pass launches
+// lost (cfg2 -3%), so the C0 kernels keep the unit loads. -DVCRC_ILV16=0
+// builds the unit loads everywhere (A/B).
 #ifndef VCRC_ILV16
 #define VCRC_ILV16 1
 #endif
 template <int GT>
 constexpr bool ilv_lanes() { return VCRC_ILV16 && (GT == 2 || GT == 4); }
+// Not in the ragged kernel (run-time G per length class): choosing the load
+// shape per item (wave-uniform branches in the round loop) cost the ragged
+// path 4-11% (u1100 ragged -11%, u600 -4%, cfg5 -10%;
+// profiles/r04_ab_ilv16_ragged.log).
 
 __device__ __forceinline__ void load_ilv(uint32_t (&w)[kWords], gu8 *span_lane, int G)  // span_lane = span + 16 g
 {
@@ -358,7 +363,7 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 struct NoMid {
     __device__ void operator()() const {}
 };
-template <int GT, int PF, bool PAY, bool BF, bool C0 = false, typename Pre, typename Mid = NoMid>
+template <int GT, int PF, bool PAY, bool BF, bool C0 = false, bool DEFER = false, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
@@ -516,7 +521,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
                 if (j < tb) acc = byte_step(acc, tail[j], sb);
         }
         const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc) p.out_crc[f] = crc;
+        if (p.out_crc && !DEFER) p.out_crc[f] = crc;  // DEFER: the caller stores it later (PendingCrc)
         if (PAY) {
             // RX rolling file CRC by-product (reference src/val_receiver.c:794,
             // 891): payload register from zero = frame register ^ (register
@@ -575,15 +580,45 @@ __device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lan
 // the static deal is kept.
 // One frame group of a uniform wave: hash group f.., fetch the next group's
 // descriptors meanwhile, advance.
+// Deferred trailer-CRC store (VCRC_DEFER_STORE, A/B): a group's CRCs are
+// stored once the next group's first loads are issued (in its pre() hook),
+// not between the group's last round and the next group's loads, so the next
+// group's first wait on the in-order vector-memory counter does not also
+// wait for the store to complete.
+#ifndef VCRC_DEFER_STORE
+#define VCRC_DEFER_STORE 0
+#endif
+struct PendingCrc {
+    uint64_t f = 0;
+    uint32_t crc = 0;
+    bool v = false;
+    __device__ __forceinline__ void flush(const FrameParams &p)
+    {
+        if (v && p.out_crc) p.out_crc[f] = crc;
+        v = false;
+    }
+    __device__ __forceinline__ void set(const FrameParams &p, uint64_t fr, bool lane_out, uint32_t acc)
+    {
+        v = lane_out;
+        f = fr;
+        crc = acc ^ p.xorout;
+    }
+};
+
 template <int G, int PF, bool PAY, bool C0, typename Pre>
 __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
-                                           uint64_t step, int lane, const SliceBases &sb, Pre &&pre)
+                                           uint64_t step, int lane, const SliceBases &sb, PendingCrc &pend, Pre &&pre)
 {
+    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
     const uint64_t fn = f + step;
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    hash_frame<G, PF, PAY, false, C0>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
+    const uint32_t acc = hash_frame<G, PF, PAY, false, C0, DEF>(p, f, f < p.n, off, L, lane % G, sb, G, [&] {
+        pre();
+        if (DEF) pend.flush(p);
+    });
+    if (DEF) pend.set(p, f, f < p.n && lane % G == G - 1, acc);
     f = fn;
     off = off_n;
     L = L_n;
@@ -618,7 +653,9 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loop.
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
-    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
+    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
+    PendingCrc pend;
+    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [&cim, &cpim] {
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
@@ -627,7 +664,8 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         VCRC_STAMP(1);
     });
     if (!p.qhead) {
-        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
+        if (DEF) pend.flush(p);
         VCRC_STAMP(2);
         return;
     }
@@ -640,7 +678,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // groups keep one word, which evens the end out better. The last wave out
     // re-zeroes the heads for the next launch on this stream.
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
-    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
     const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
     // the lane id again from mbcnt: kept live from the entry, it was the one
     // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
@@ -666,7 +704,10 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
             uint64_t od = 0;
             uint32_t Ld = 0;
             if (fd < p.n) frame_desc(p, fd, od, Ld);
-            hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
+            const uint32_t acc = hash_frame<G, PF, PAY, false, C0, DEF>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [&] {
+                if (DEF) pend.flush(p);
+            });
+            if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
         }
     }
     uint32_t k = 0;
@@ -680,16 +721,23 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         if (ql == 0) kn = atomicAdd(&p.qhead[part * 16u], 1u);
         uint64_t gb_n = 0, fd_n = 0, od_n = 0;
         uint32_t Ld_n = 0;
-        hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {}, [&] {
-            gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
-            fd_n = gb_n + (uint64_t)(ql / G);
-            if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
-        });
+        const uint32_t acc = hash_frame<G, PF, PAY, false, C0, DEF>(
+            p, fd, fd < p.n, od, Ld, ql % G, sb, G,
+            [&] {
+                if (DEF) pend.flush(p);
+            },
+            [&] {
+                gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
+                fd_n = gb_n + (uint64_t)(ql / G);
+                if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
+            });
+        if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
         gb = gb_n;
         fd = fd_n;
         od = od_n;
         Ld = Ld_n;
     }
+    if (DEF) pend.flush(p);
     VCRC_STAMP(2);
     if (ql == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
