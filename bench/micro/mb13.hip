@@ -21,6 +21,9 @@
 //              flight, as the product does
 //   ilv16      (round 4) the frames pattern read as a 16-B interleave:
 //              instruction q covers G x 16 contiguous bytes of each frame
+//   bidir      (round 4) odd frames read their rounds last first
+// Frames start 512 B into the buffer: round 0's span starts before its
+// frame (the 16-B interleave reads it whole).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -91,7 +94,12 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
         // product: no unrolled, hoisted rounds); 128 = the 16-B interleave
         // (round span read as four instructions of G x 16 contiguous bytes
         // per frame, lane g at 16 g; mb14)
-        constexpr bool DESC = MODE & 8, ST = MODE & 16, SH = MODE & 32, RTL = MODE & 64, ILV = MODE & 128;
+        // 256 (with 128) = bidirectional: odd frames read their rounds last
+        // first, so both sides of every frame boundary are read in the same
+        // round (the boundary line is otherwise fetched twice, R - 1 rounds
+        // apart: 1.12x traffic on 1,100-B frames)
+        constexpr bool DESC = MODE & 8, ST = MODE & 16, SH = MODE & 32, RTL = MODE & 64, ILV = MODE & 128,
+                       BIDIR = MODE & 256;
         const int g = lane % kG;
         uint32_t nL = 0;  // DESC: the next group's descriptors, fetched while this group is read (as k_frames does)
         uint64_t noff = 0;
@@ -117,10 +125,13 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
             gu8 *fp = (gu8 *)base + off;
             const int u0 = (int)U - (int)(kG * R) + g;
             u32x4u w0[4], nx[4];
-            if (ILV) {  // round r's span starts at fp + 64 (U - G R + G r) - pad; lane g at 16 g + 16 G q
-                gu8 *sp = fp + (int64_t)((int)U - (int)(kG * R)) * 64 - pad + 16 * g;
-                if (R > 0) ld64i(w0, sp);
-                if (R > 1) ld64i(nx, sp + kG * 64);
+            // round r's span starts at fp + 64 (U - G R + G r) - pad; lane g at 16 g + 16 G q
+            gu8 *sp0 = fp + (int64_t)((int)U - (int)(kG * R)) * 64 - pad + 16 * g;
+            const bool back = BIDIR && (f & 1);
+            auto span = [&](uint32_t r) { return sp0 + (int64_t)(back ? R - 1 - r : r) * kG * 64; };
+            if (ILV) {
+                if (R > 0) ld64i(w0, span(0));
+                if (R > 1) ld64i(nx, span(1));
             } else {
                 if (R > 0 && u0 >= 0) {
                     const uint32_t inl = (uint32_t)((uintptr_t)fp & 127u);
@@ -144,7 +155,7 @@ __global__ __launch_bounds__(1024) void k_pat(const uint8_t *base, uint64_t byte
 #pragma unroll
                 for (int q = 0; q < 4; q++) cur[q] = nx[q];
                 if (r + 1 < R) {
-                    if (ILV) ld64i(nx, up + (uint64_t)r * kG * 64);
+                    if (ILV) ld64i(nx, span(r + 1));
                     else ld64(nx, up + (uint64_t)r * kG * 64);
                 }
                 a = (a << 1 | a >> 31) ^ xr(cur);
@@ -228,7 +239,7 @@ int main()
     const double crc_bytes = (double)kN * kL;
 #define RUN(M, name)                                                                                                 \
     {                                                                                                                \
-        const float ms = timeit([&] { hipLaunchKernelGGL((k_pat<M>), dim3(cus), dim3(1024), 0, 0, d, bytes, out, doff, dlen, outf, kL); }); \
+        const float ms = timeit([&] { hipLaunchKernelGGL((k_pat<M>), dim3(cus), dim3(1024), 0, 0, d + 512, bytes, out, doff, dlen, outf, kL); }); \
         printf("%-9s %.4f ms  %7.1f GB/s of CRC input (%llu x %u B)  %7.1f GB/s of buffer\n", name, ms,                \
                crc_bytes / ms / 1e6, (unsigned long long)kN, kL, (double)bytes / ms / 1e6);                            \
         fflush(stdout);                                                                                              \
@@ -236,9 +247,9 @@ int main()
     for (int rep = 0; rep < 2; rep++) {
         RUN(64, "frames rtL")
         RUN(64 + 128, "ilv16 rtL")
-        RUN(64 + 16, "frames rtL st")
-        RUN(64 + 128 + 16, "ilv16 rtL st")
+        RUN(64 + 128 + 256, "ilv16 rtL bidir")
         RUN(128, "ilv16")
+        RUN(128 + 256, "ilv16 bidir")
         RUN(0, "frames")
         RUN(8, "+desc")
         RUN(24, "+desc+st")
