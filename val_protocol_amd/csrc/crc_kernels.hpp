@@ -363,7 +363,7 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 struct NoMid {
     __device__ void operator()() const {}
 };
-template <int GT, int PF, bool PAY, bool BF, bool C0 = false, typename Pre, typename Mid = NoMid>
+template <int GT, int PF, bool PAY, bool BF, bool C0 = false, bool DEFER = false, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
@@ -521,7 +521,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
                 if (j < tb) acc = byte_step(acc, tail[j], sb);
         }
         const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc) p.out_crc[f] = crc;
+        if (p.out_crc && !DEFER) p.out_crc[f] = crc;  // DEFER: the caller stores it later (PendingCrc)
         if (PAY) {
             // RX rolling file CRC by-product (reference src/val_receiver.c:794,
             // 891): payload register from zero = frame register ^ (register
@@ -547,37 +547,38 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
 
 // ---- bidirectional frames (k_frames at G = 2 and 4, PF = 1) -----------------
 // Frames are packed back to back, so the 128-B line holding a frame's last
-// bytes also holds the next frame's first bytes. Hashed first round first by
-// one wave in lockstep, frame i reads that line in its last round and frame
-// i + 1 in its round 0, R - 1 rounds earlier: at 1,100 B (R = 5) about 13 us,
-// longer than the L2 keeps a line at the full stream rate, so every boundary
-// line came from HBM twice (1.12x traffic on 1,100-B frames, 1.35x on 600-B,
-// 1.19x on cfg2; profiles/r03_pmc_short.json).
-// Here the frames of a block of 2 x 64/G consecutive frames are split by
-// parity over a pair of adjacent waves: the even frames run forward on one,
-// the odd frames last round first on the other, so frame 2j's end and frame
-// 2j + 1's start are read in the same round (both waves' last), and frame
-// 2j + 1's end and 2j + 2's start as well (both waves' round 0). The
-// direction is wave-uniform: a first version that mixed directions inside a
-// wave ran every divergent section twice and lost 7-25%
-// (profiles/r04_ab_bidir_short.log; branch exp/bd4).
+// bytes also holds the next frame's first bytes. Hashed first round first,
+// frame i reads that line in its last round and frame i + 1 in its round 0,
+// R - 1 rounds earlier (the same wave hashes both in lockstep): at 1,100 B
+// (R = 5) that is ~13 us, longer than the L2 keeps a line at full stream
+// rate, so every boundary line came from HBM twice (1.12x traffic on
+// 1,100-B frames, 1.35x on 600-B, 1.19x on cfg2; profiles/r03_pmc_short.json).
+// Here odd frames are hashed last round first: frame 2i and 2i + 1 read
+// their shared line in the same round (2i's last, 2i+1's first), and 2i + 1
+// and 2i + 2 in the same round (2i+1's last, covering its start, and 2i+2's
+// round 0). A group holds an even number of frames and adjacent groups go to
+// adjacent waves, so group edges pair up the same way. (mb13 XOR-only read
+// shape: 1.227x -> 1.038x traffic, +4.5%, profiles/r04_micro_mb13_bidir.log;
+// at G >= 8 the boundary is a small share of each frame and descending
+// streams cost 6-12%, profiles/r03_ab_bidirectional.log, so long frames keep
+// the forward order.)
 // A backward lane keeps B_k = H_k ^ M^-1 B_(k+1), k = R-1 .. 0 (H_k: its
 // round-k unit's register from zero; M^-1 = "advance -G 64 bytes", one LDS
 // nibble map, back_map), and M^(R-1) B_0 = sum M^(R-1-k) H_k is the forward
 // register: one variable shift (LDS pow maps) at the end. Rounds >= 1 use the
-// 16-B interleaved loads; a backward frame's round 0 (unit 0, the frame's
-// first line, with the header words) comes last and is read by the line
-// loads; its end dwords (tail bytes, trailer) are read with its first round,
-// when that line is read anyway.
+// 16-B interleaved loads; a backward lane's round 0 (unit 0, the frame's
+// first line) comes last and is read by the line loads; the frame's end
+// dwords (tail bytes, trailer) are read with its first round, when that line
+// is read anyway.
 #ifndef VCRC_BIDIR
 #define VCRC_BIDIR 1
 #endif
 template <int G, int PF, bool PAY>
 constexpr bool bidir_frames() { return VCRC_BIDIR && !PAY && PF == 1 && (G == 2 || G == 4); }
 
-template <int GT, bool C0, typename Pre, typename Mid>
+template <int GT, bool C0, bool DEFER, typename Pre, typename Mid>
 __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L,
-                                                  int g, const SliceBases &sb, bool backward, Pre &&pre, Mid &&mid)
+                                                  int g, const SliceBases &sb, Pre &&pre, Mid &&mid)
 {
     static_assert(GT == 2 || GT == 4, "bidirectional frames: G = 2 or 4");
     constexpr int G = GT, lgG = ilog2(GT);
@@ -592,15 +593,13 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
     const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
     const uint64_t kStep = (uint64_t)G * kUnit;
     gu8 *const span_lane = fp + (int64_t)((int)U - G * (int)R) * kUnit - pad + 16 * g;  // round 0's span + 16 g
-    const bool bwd = backward && R >= 2u;  // wave-uniform but for a batch's last, shorter frame
+    const bool bwd = (f & 1u) && R >= 2u;
     const bool last_lane = active && g == G - 1;
     gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
     const bool tiny = u0 == 0 && Lg < 4;
-    const bool hdr = R > 0 && u0 == 0 && p.out_hdr;
     // step 0: forward round 0 (unit 0), backward round R - 1
     uint32_t w0[kWords];
     uint32_t e0 = 0, e1 = 0;  // backward: the dwords at the grid end (tail bytes, trailer)
-    uint32_t h0 = 0, h1 = 0;  // header words (backward: loaded with round 0, at the end)
     if (bwd) {
         load_ilv(w0, span_lane + (uint64_t)(R - 1) * kStep, G);
         if (last_lane) {
@@ -609,21 +608,16 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
         }
     } else {
         load_unit0<false, C0>(w0, u0, fp, Lg, pad, dummy);
-        if (hdr && L >= 8) {
-            h0 = ld32(fp);
-            h1 = ld32(fp + 4);
-        }
+    }
+    const bool hdr = R > 0 && u0 == 0 && p.out_hdr;
+    uint32_t h0, h1;
+    if (hdr && L >= 8) {
+        h0 = ld32(fp);
+        h1 = ld32(fp + 4);
     }
     uint32_t nxt[kWords];
-    auto load_round0_bwd = [&](uint32_t (&w)[kWords]) {
-        load_unit0<false, false>(w, u0, fp, Lg, pad, dummy);
-        if (hdr && L >= 8) {
-            h0 = ld32(fp);
-            h1 = ld32(fp + 4);
-        }
-    };
     if (R > 1) {
-        if (bwd && R == 2) load_round0_bwd(nxt);
+        if (bwd && R == 2) load_unit0<false, false>(nxt, u0, fp, Lg, pad, dummy);
         else load_ilv(nxt, span_lane + (uint64_t)(bwd ? R - 2 : 1u) * kStep, G);
     }
     int first = bwd ? 0 : ((R == 0 || u0 < 0) ? kWords : (u0 == 0 ? (int)(pad >> 2) : 0));
@@ -631,19 +625,16 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
     for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
     first = __builtin_amdgcn_readfirstlane(first);
     pre();
-    auto put_hdr = [&] {
-        if (hdr) {
-            uint32_t h = seed;
-            if (L >= 8) {
-                h = s4_step(h, h0, sb);
-                h = s4_step(h, h1, sb);
-            } else {
-                for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
-            }
-            p.out_hdr[f] = h ^ p.xorout;
+    if (hdr) {
+        uint32_t h = seed;
+        if (L >= 8) {
+            h = s4_step(h, h0, sb);
+            h = s4_step(h, h1, sb);
+        } else {
+            for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
         }
-    };
-    if (!bwd) put_hdr();
+        p.out_hdr[f] = h ^ p.xorout;
+    }
     // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, round 1).
     const bool seed_spill = g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1;
     const uint32_t spill = seed >> (8 * (kUnit - pad));
@@ -665,41 +656,37 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
     mid();
     // steps 1 .. R-1 (forward) or 1 .. R-2 (backward: its round 0 is peeled below)
     const uint32_t tend = bwd ? R - 1 : R;
-    const uint32_t rmap = bwd ? bmap : gmap;
     for (uint32_t t = 1; t < tend; t++) {
         uint32_t w[kWords];
 #pragma unroll
         for (int i = 0; i < kWords; i++) w[i] = nxt[i];
         if (t + 1 < R) {
             const uint32_t kn = bwd ? R - 2 - t : t + 1;
-            if (bwd && kn == 0) load_round0_bwd(nxt);
+            if (bwd && kn == 0) load_unit0<false, false>(nxt, u0, fp, Lg, pad, dummy);
             else load_ilv(nxt, span_lane + (uint64_t)kn * kStep, G);
         }
         ilv_to_units<GT>(w, g);
         if ((bwd ? R - 1 - t : t) == 1u && seed_spill) w[0] ^= spill;
-        const uint32_t mp = map_apply(acc, rmap);
+        const uint32_t mp = map_apply(acc, bwd ? bmap : gmap);
         uint32_t c = bwd ? 0u : mp;
 #pragma unroll
         for (int i = 0; i < kWords; i++) c = s4_step(c, w[i], sb);
         acc = bwd ? c ^ mp : c;
     }
-    // backward frames: round 0, the start of the frame (masked, seeded), then
+    // backward lanes: round 0, the start of the frame (masked, seeded), then
     // the register is advanced over the (R - 1) G 64 bytes after round 0
-    if (backward) {  // wave-uniform
-        int first0 = (bwd && u0 >= 0) ? (u0 == 0 ? (int)(pad >> 2) : 0) : kWords;
+    int first0 = (bwd && u0 >= 0) ? (u0 == 0 ? (int)(pad >> 2) : 0) : kWords;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) first0 = min(first0, __shfl_xor(first0, o));
-        first0 = __builtin_amdgcn_readfirstlane(first0);
-        if (bwd) {
-            uint32_t w[kWords];
+    for (int o = 1; o < 64; o <<= 1) first0 = min(first0, __shfl_xor(first0, o));
+    first0 = __builtin_amdgcn_readfirstlane(first0);
+    if (bwd) {
+        uint32_t w[kWords];
 #pragma unroll
-            for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-            if (u0 == 0 && Lg >= 4) unit0_line_shift(w, fp, pad);
-            unit0_finish(w, u0, Lg, pad, seed);
-            acc = s4_words_from(first0, w, sb) ^ map_apply(acc, bmap);
-            acc = shift_bytes(acc, (R - 1u) << (6 + lgG), p.consts);
-            put_hdr();
-        }
+        for (int i = 0; i < kWords; i++) w[i] = nxt[i];
+        if (u0 == 0 && Lg >= 4) unit0_line_shift(w, fp, pad);
+        unit0_finish(w, u0, Lg, pad, seed);
+        acc = s4_words_from(first0, w, sb) ^ map_apply(acc, bmap);
+        acc = shift_bytes(acc, (R - 1u) << (6 + lgG), p.consts);
     }
     uint32_t tail[3] = {0, 0, 0}, trailer = 0;
     if (last_lane) {
@@ -730,7 +717,7 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
                 if (j < tb) acc = byte_step(acc, tail[j], sb);
         }
         const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc) p.out_crc[f] = crc;
+        if (p.out_crc && !DEFER) p.out_crc[f] = crc;
         if (p.verify) {
             const bool good = (crc == trailer);
             if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
@@ -740,16 +727,16 @@ __device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t
     return acc;
 }
 
-// The frames kernel's per-group hash: bidirectional at G = 2 and 4 (PF = 1,
-// no payload states), else hash_frame (backward ignored).
-template <int G, int PF, bool PAY, bool C0, typename Pre, typename Mid = NoMid>
+// The frames kernels' per-group hash: bidirectional at G = 2 and 4 (PF = 1,
+// no payload states), else hash_frame.
+template <int G, int PF, bool PAY, bool C0, bool DEFER, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t frame_hash(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           const SliceBases &sb, bool backward, Pre &&pre, Mid &&mid = Mid{})
+                                           const SliceBases &sb, Pre &&pre, Mid &&mid = Mid{})
 {
     if constexpr (bidir_frames<G, PF, PAY>())
-        return hash_frame_bd<G, C0>(p, f, active, off, L, g, sb, backward, pre, mid);
+        return hash_frame_bd<G, C0, DEFER>(p, f, active, off, L, g, sb, pre, mid);
     else
-        return hash_frame<G, PF, PAY, false, C0>(p, f, active, off, L, g, sb, G, pre, mid);
+        return hash_frame<G, PF, PAY, false, C0, DEFER>(p, f, active, off, L, g, sb, G, pre, mid);
 }
 
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
@@ -787,15 +774,45 @@ __device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lan
 // the static deal is kept.
 // One frame group of a uniform wave: hash group f.., fetch the next group's
 // descriptors meanwhile, advance.
+// Deferred trailer-CRC store (VCRC_DEFER_STORE, A/B): a group's CRCs are
+// stored once the next group's first loads are issued (in its pre() hook),
+// not between the group's last round and the next group's loads, so the next
+// group's first wait on the in-order vector-memory counter does not also
+// wait for the store to complete.
+#ifndef VCRC_DEFER_STORE
+#define VCRC_DEFER_STORE 0
+#endif
+struct PendingCrc {
+    uint64_t f = 0;
+    uint32_t crc = 0;
+    bool v = false;
+    __device__ __forceinline__ void flush(const FrameParams &p)
+    {
+        if (v && p.out_crc) p.out_crc[f] = crc;
+        v = false;
+    }
+    __device__ __forceinline__ void set(const FrameParams &p, uint64_t fr, bool lane_out, uint32_t acc)
+    {
+        v = lane_out;
+        f = fr;
+        crc = acc ^ p.xorout;
+    }
+};
+
 template <int G, int PF, bool PAY, bool C0, typename Pre>
 __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
-                                           uint64_t step, int lane, const SliceBases &sb, bool backward, Pre &&pre)
+                                           uint64_t step, int lane, const SliceBases &sb, PendingCrc &pend, Pre &&pre)
 {
+    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
     const uint64_t fn = f + step;
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    frame_hash<G, PF, PAY, C0>(p, f, f < p.n, off, L, lane % G, sb, backward, pre);
+    const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(p, f, f < p.n, off, L, lane % G, sb, [&] {
+        pre();
+        if (DEF) pend.flush(p);
+    });
+    if (DEF) pend.set(p, f, f < p.n && lane % G == G - 1, acc);
     f = fn;
     off = off_n;
     L = L_n;
@@ -812,24 +829,17 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
     const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;  // even: 16 per workgroup
-    // Group q's frames: q * 64/G + 0, 1, ..., or with bidirectional frames
-    // every other frame of block q / 2 (2 x 64/G frames), the odd ones (odd q)
-    // backward; adjacent waves take groups q, q + 1 of one block.
-    constexpr bool BD = bidir_frames<G, PF, PAY>();
-    constexpr uint64_t kFS = BD ? 2 : 1;  // frame stride inside a group
-    auto gfirst = [](uint64_t q) -> uint64_t { return BD ? (q >> 1) * (2 * kGroups) + (q & 1) : q * kGroups; };
+    const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
     LdsImage im;
     lds_tables_issue(p.consts, im);
     PowImage pim;
-    constexpr bool POW = PAY || BD;  // payload states; backward frames' final shift
+    constexpr bool POW = PAY || bidir_frames<G, PF, PAY>();  // payload states, backward frames' final shift
     if (POW) lds_pow_issue(p.consts, 0, pim);
     // Descriptors of the next frame group are fetched while this one hashes.
     // (Loading the first group's descriptors branch-free before the blob, so
     // the prologue overlaps the first frame loads exactly, measured slower:
     // cfg2 -3%, 256-frame windows -9%, cfg3 -1%.)
-    uint64_t fb = gfirst(wave), f = fb + kFS * (uint64_t)(lane / G), off = 0;
-    const bool wave_back = BD && (wave & 1);  // the static deal keeps a wave's parity (nwaves is even)
+    uint64_t fb = wave * kGroups, f = fb + (uint64_t)(lane / G), off = 0;
     uint32_t L = 0;
     if (f < p.n) frame_desc(p, f, off, L);
     // Every wave runs the first pass (lanes past the batch hash nothing): the
@@ -838,7 +848,9 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loop.
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
-    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, wave_back, [&cim, &cpim] {
+    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
+    PendingCrc pend;
+    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [&cim, &cpim] {
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
@@ -847,7 +859,8 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         VCRC_STAMP(1);
     });
     if (!p.qhead) {
-        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, wave_back, [] {});
+        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
+        if (DEF) pend.flush(p);
         VCRC_STAMP(2);
         return;
     }
@@ -860,8 +873,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // groups keep one word, which evens the end out better. The last wave out
     // re-zeroes the heads for the next launch on this stream.
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
-    while (fb < p.n && fb < dyn)
-        group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, wave_back, [] {});
+    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
     const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
     // the lane id again from mbcnt: kept live from the entry, it was the one
     // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
@@ -881,39 +893,46 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
             uint32_t k = 0;
             if (ql == 0) k = atomicAdd(&p.qhead[0], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            const uint64_t gb = dyn + gfirst(k);  // dyn is a whole number of blocks
+            const uint64_t gb = dyn + (uint64_t)k * kGroups;
             if (gb >= p.n) break;
-            const uint64_t fd = gb + kFS * (uint64_t)(ql / G);
+            const uint64_t fd = gb + (uint64_t)(ql / G);
             uint64_t od = 0;
             uint32_t Ld = 0;
             if (fd < p.n) frame_desc(p, fd, od, Ld);
-            frame_hash<G, PF, PAY, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, BD && (k & 1u), [] {});
+            const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(p, fd, fd < p.n, od, Ld, ql % G, sb, [&] {
+                if (DEF) pend.flush(p);
+            });
+            if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
         }
     }
     uint32_t k = 0;
     if (P > 1u && ql == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
-    uint64_t q = (uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(k);  // group index in the queue
-    uint64_t gb = P == 1u ? p.n : dyn + gfirst(q);
-    uint64_t fd = gb + kFS * (uint64_t)(ql / G), od = 0;
+    uint64_t gb = P == 1u ? p.n : dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(k)) * kGroups;
+    uint64_t fd = gb + (uint64_t)(ql / G), od = 0;
     uint32_t Ld = 0;
     if (fd < p.n) frame_desc(p, fd, od, Ld);
     while (gb < p.n) {
         uint32_t kn = 0;
         if (ql == 0) kn = atomicAdd(&p.qhead[part * 16u], 1u);
-        uint64_t q_n = 0, gb_n = 0, fd_n = 0, od_n = 0;
+        uint64_t gb_n = 0, fd_n = 0, od_n = 0;
         uint32_t Ld_n = 0;
-        frame_hash<G, PF, PAY, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, BD && (q & 1u), [] {}, [&] {
-            q_n = (uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn);
-            gb_n = dyn + gfirst(q_n);
-            fd_n = gb_n + kFS * (uint64_t)(ql / G);
-            if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
-        });
-        q = q_n;
+        const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(
+            p, fd, fd < p.n, od, Ld, ql % G, sb,
+            [&] {
+                if (DEF) pend.flush(p);
+            },
+            [&] {
+                gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
+                fd_n = gb_n + (uint64_t)(ql / G);
+                if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
+            });
+        if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
         gb = gb_n;
         fd = fd_n;
         od = od_n;
         Ld = Ld_n;
     }
+    if (DEF) pend.flush(p);
     VCRC_STAMP(2);
     if (ql == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
