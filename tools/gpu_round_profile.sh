@@ -22,5 +22,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_v -o p -- python3 $R/tools/prof_target.py cfg3 3 verify > $O/pmc_fetch_v.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch5 -o p -- python3 $R/tools/prof_target.py cfg5 3 > $O/pmc_fetch5.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write5 -o p -- python3 $R/tools/prof_target.py cfg5 3 > $O/pmc_write5.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -o p -- python3 $R/tools/prof_target.py cfg3 3 > $O/pmc_sq.log 2>&1 && \
+cd $R && bash tools/pmc_short.sh u1100d cfg2 > $O/pmc_short.log 2>&1
 echo "round profile rc=$?"
+# short-frame PMC passes land in gpurun_out/pmcs: python tools/pmc_short_summary.py > profiles/rNN_pmc_short.json
