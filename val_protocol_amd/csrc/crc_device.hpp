@@ -7,14 +7,13 @@
 //   [0, 128 KiB)        slice tables T3|T2 (pair 0) and T1|T0 (pair 1):
 //                       row = byte value * 256 B, half = 128 B, 32 bank replicas
 //                       of 4 B, so the 32 lanes of a half-wave read 32 banks.
-//   [128 KiB, +7.5 KiB) 15 nibble maps of 512 B, one copy each: gap maps
+//   [128 KiB, +6.5 KiB) 13 nibble maps of 512 B, one copy each: gap maps
 //                       "advance (G - 1) * 64 bytes" for G = 2^0..2^6, then
-//                       merge maps "advance 64 * 2^j bytes", j = 0..5, then
-//                       back maps "advance -G * 64 bytes", G = 2, 4. A map is
+//                       merge maps "advance 64 * 2^j bytes", j = 0..5. A map is
 //                       8 tables x 16 words; a lookup of nibble k reads one of
 //                       16 consecutive words, so lanes either share a word
 //                       (broadcast) or hit distinct banks: no replicas needed.
-//   [135.5 KiB, +8 KiB) 16 nibble maps "advance 2^(k0+i) bytes", i = 0..15:
+//   [134.5 KiB, +8 KiB) 16 nibble maps "advance 2^(k0+i) bytes", i = 0..15:
 //                       k0 = 0 for the variable shift of the RX payload-state
 //                       by-product, k0 = log2(chunk) for the region fold
 //                       (filled only by launches that use them).
@@ -45,7 +44,7 @@ constexpr int kBlock = 1024;           // threads per workgroup (16 waves, 1 wor
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kLdsS4 = 0;
 constexpr uint32_t kLdsMaps = 131072;
-constexpr uint32_t kNumMaps = 7 + 6 + 2;  // gap maps G = 2^0..2^6, merge maps j = 0..5, back maps G = 2, 4
+constexpr uint32_t kNumMaps = 7 + 6;   // gap maps G = 2^0..2^6, merge maps j = 0..5
 constexpr uint32_t kNumPowMaps = 16;   // LDS slots of "advance 2^(k0+i) bytes"
 constexpr uint32_t kBlobPowMaps = 48;  // blob maps "advance 2^k bytes", k = 0..47
 constexpr uint32_t kLdsPow = kLdsMaps + kNumMaps * 512;
@@ -122,9 +121,6 @@ __device__ __forceinline__ uint32_t map_apply(uint32_t a, uint32_t map)
 }
 __host__ __device__ constexpr uint32_t gap_map(int gi) { return kLdsMaps + (uint32_t)gi * 512u; }
 __host__ __device__ constexpr uint32_t tree_map(int j) { return kLdsMaps + (7u + (uint32_t)j) * 512u; }
-// "advance -G * 64 bytes" (x^(-8 G 64) = x^(8 (2^32 - 1 - 64 G)): x has order
-// 2^32 - 1 mod P) for G = 2^gi, gi = 1, 2: the backward frames' round step
-__host__ __device__ constexpr uint32_t back_map(int gi) { return kLdsMaps + (13u + (uint32_t)gi - 1u) * 512u; }
 __host__ __device__ constexpr uint32_t pow_map(int k) { return kLdsPow + (uint32_t)k * 512u; }
 
 // Device constant blob (u32 words, built once per device at init from
@@ -134,13 +130,11 @@ __host__ __device__ constexpr uint32_t pow_map(int k) { return kLdsPow + (uint32
 //   [kConstGap,   +7*128)  nibble map "advance (G - 1) * 64 bytes" for G = 2^i,
 //                          entry k * 16 + n = image of n << 4k
 //   [kConstTree,  +6*128)  nibble map "advance 64 * 2^j bytes" (merge level j)
-//   [kConstBack,  +2*128)  nibble map "advance -G * 64 bytes", G = 2, 4
 //   [kConstPow,  +48*128)  nibble map "advance 2^k bytes", k = 0..47
 //   [kConstPowHi,    +16)  x^(8 * 2^k) mod P for k = 16..31 (shifts past 64 KiB, VALU)
 // The maps are contiguous, in LDS order.
 constexpr uint32_t kConstSlice = 0, kConstGap = 1024, kConstTree = 1024 + 7 * 128;
-constexpr uint32_t kConstBack = kConstTree + kMaxTree * 128;
-constexpr uint32_t kConstPow = kConstBack + 2 * 128;
+constexpr uint32_t kConstPow = kConstTree + kMaxTree * 128;
 constexpr uint32_t kConstPowHi = kConstPow + kBlobPowMaps * 128;
 constexpr uint32_t kConstWords = kConstPowHi + 16;
 
@@ -252,10 +246,6 @@ __host__ inline void fill_const_blob(uint32_t *w)
     for (int j = 0; j < kMaxTree; j++) {
         const uint32_t x = gf2_x8n((uint64_t)kUnit << j);
         for (int t = 0; t < 128; t++) w[kConstTree + j * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
-    }
-    for (int gi = 1; gi <= 2; gi++) {
-        const uint32_t x = gf2_x8n(0xFFFFFFFFull - ((uint64_t)kUnit << gi));
-        for (int t = 0; t < 128; t++) w[kConstBack + (gi - 1) * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
     }
     for (int k = 0; k < (int)kBlobPowMaps; k++) {
         const uint32_t x = gf2_x8n((uint64_t)1 << k);

@@ -363,7 +363,7 @@ __device__ __forceinline__ uint32_t s4_words_from(int first, const uint32_t (&w)
 struct NoMid {
     __device__ void operator()() const {}
 };
-template <int GT, int PF, bool PAY, bool BF, bool C0 = false, bool DEFER = false, typename Pre, typename Mid = NoMid>
+template <int GT, int PF, bool PAY, bool BF, bool C0 = false, typename Pre, typename Mid = NoMid>
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
@@ -521,7 +521,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
                 if (j < tb) acc = byte_step(acc, tail[j], sb);
         }
         const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc && !DEFER) p.out_crc[f] = crc;  // DEFER: the caller stores it later (PendingCrc)
+        if (p.out_crc) p.out_crc[f] = crc;
         if (PAY) {
             // RX rolling file CRC by-product (reference src/val_receiver.c:794,
             // 891): payload register from zero = frame register ^ (register
@@ -543,200 +543,6 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
         }
     }
     return acc;  // lane G - 1: the frame's raw register (before xorout)
-}
-
-// ---- bidirectional frames (k_frames at G = 2 and 4, PF = 1) -----------------
-// Frames are packed back to back, so the 128-B line holding a frame's last
-// bytes also holds the next frame's first bytes. Hashed first round first,
-// frame i reads that line in its last round and frame i + 1 in its round 0,
-// R - 1 rounds earlier (the same wave hashes both in lockstep): at 1,100 B
-// (R = 5) that is ~13 us, longer than the L2 keeps a line at full stream
-// rate, so every boundary line came from HBM twice (1.12x traffic on
-// 1,100-B frames, 1.35x on 600-B, 1.19x on cfg2; profiles/r03_pmc_short.json).
-// Here odd frames are hashed last round first: frame 2i and 2i + 1 read
-// their shared line in the same round (2i's last, 2i+1's first), and 2i + 1
-// and 2i + 2 in the same round (2i+1's last, covering its start, and 2i+2's
-// round 0). A group holds an even number of frames and adjacent groups go to
-// adjacent waves, so group edges pair up the same way. (mb13 XOR-only read
-// shape: 1.227x -> 1.038x traffic, +4.5%, profiles/r04_micro_mb13_bidir.log;
-// at G >= 8 the boundary is a small share of each frame and descending
-// streams cost 6-12%, profiles/r03_ab_bidirectional.log, so long frames keep
-// the forward order.)
-// A backward lane keeps B_k = H_k ^ M^-1 B_(k+1), k = R-1 .. 0 (H_k: its
-// round-k unit's register from zero; M^-1 = "advance -G 64 bytes", one LDS
-// nibble map, back_map), and M^(R-1) B_0 = sum M^(R-1-k) H_k is the forward
-// register: one variable shift (LDS pow maps) at the end. Rounds >= 1 use the
-// 16-B interleaved loads; a backward lane's round 0 (unit 0, the frame's
-// first line) comes last and is read by the line loads; the frame's end
-// dwords (tail bytes, trailer) are read with its first round, when that line
-// is read anyway.
-#ifndef VCRC_BIDIR
-#define VCRC_BIDIR 1
-#endif
-template <int G, int PF, bool PAY>
-constexpr bool bidir_frames() { return VCRC_BIDIR && !PAY && PF == 1 && (G == 2 || G == 4); }
-
-template <int GT, bool C0, bool DEFER, typename Pre, typename Mid>
-__device__ __forceinline__ uint32_t hash_frame_bd(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L,
-                                                  int g, const SliceBases &sb, Pre &&pre, Mid &&mid)
-{
-    static_assert(GT == 2 || GT == 4, "bidirectional frames: G = 2 or 4");
-    constexpr int G = GT, lgG = ilog2(GT);
-    const uint32_t gmap = gap_map(lgG), bmap = back_map(lgG);
-    gu8 *fp = gptr(p.base) + off;
-    const uint32_t seed = (f == 0) ? p.seed0 : p.seed_rest;
-    const uint32_t tb = min((uint32_t)((uintptr_t)(fp + L) & 3u), L);
-    const uint32_t Lg = L - tb;
-    const uint32_t U = Lg ? (Lg + kUnit - 1) / kUnit : 1u;
-    const uint32_t R = active ? (U + G - 1) >> lgG : 0u;
-    const uint32_t pad = U * kUnit - Lg;
-    const int u0 = (int)U - G * (int)R + g;  // this lane's unit in round 0
-    const uint64_t kStep = (uint64_t)G * kUnit;
-    gu8 *const span_lane = fp + (int64_t)((int)U - G * (int)R) * kUnit - pad + 16 * g;  // round 0's span + 16 g
-    const bool bwd = (f & 1u) && R >= 2u;
-    const bool last_lane = active && g == G - 1;
-    gu8 *const dummy = gptr(reinterpret_cast<const uint8_t *>(p.consts));
-    const bool tiny = u0 == 0 && Lg < 4;
-    // step 0: forward round 0 (unit 0), backward round R - 1
-    uint32_t w0[kWords];
-    uint32_t e0 = 0, e1 = 0;  // backward: the dwords at the grid end (tail bytes, trailer)
-    if (bwd) {
-        load_ilv(w0, span_lane + (uint64_t)(R - 1) * kStep, G);
-        if (last_lane) {
-            if (tb || p.verify) e0 = ld32(fp + Lg);  // dword-aligned: never crosses into a page past the frame
-            if (tb && p.verify) e1 = ld32(fp + Lg + 4);
-        }
-    } else {
-        load_unit0<false, C0>(w0, u0, fp, Lg, pad, dummy);
-    }
-    const bool hdr = R > 0 && u0 == 0 && p.out_hdr;
-    uint32_t h0, h1;
-    if (hdr && L >= 8) {
-        h0 = ld32(fp);
-        h1 = ld32(fp + 4);
-    }
-    uint32_t nxt[kWords];
-    if (R > 1) {
-        if (bwd && R == 2) load_unit0<false, false>(nxt, u0, fp, Lg, pad, dummy);
-        else load_ilv(nxt, span_lane + (uint64_t)(bwd ? R - 2 : 1u) * kStep, G);
-    }
-    int first = bwd ? 0 : ((R == 0 || u0 < 0) ? kWords : (u0 == 0 ? (int)(pad >> 2) : 0));
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) first = min(first, __shfl_xor(first, o));
-    first = __builtin_amdgcn_readfirstlane(first);
-    pre();
-    if (hdr) {
-        uint32_t h = seed;
-        if (L >= 8) {
-            h = s4_step(h, h0, sb);
-            h = s4_step(h, h1, sb);
-        } else {
-            for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
-        }
-        p.out_hdr[f] = h ^ p.xorout;
-    }
-    // Seed bytes past a unit 0 with < 4 real bytes land in unit 1 (lane 0, round 1).
-    const bool seed_spill = g == 0 && pad > kUnit - 4 && (int)U - G * (int)(R - 1) == 1;
-    const uint32_t spill = seed >> (8 * (kUnit - pad));
-    uint32_t acc = 0;
-    if (R > 0) {
-        if (bwd) {
-            ilv_to_units<GT>(w0, g);
-            if (R == 2 && seed_spill) w0[0] ^= spill;  // round R - 1 is round 1
-        } else {
-            if (u0 == 0 && Lg >= 4 && !C0) unit0_line_shift(w0, fp, pad);
-            unit0_finish(w0, u0, Lg, pad, seed);
-        }
-        acc = s4_words_from(first, w0, sb);
-        if (tiny) {  // Lg < 4: state of all L bytes straight from the seed (forward: R == 1)
-            acc = seed;
-            for (uint32_t i = 0; i < L; i++) acc = byte_step(acc, fp[i], sb);
-        }
-    }
-    mid();
-    // steps 1 .. R-1 (forward) or 1 .. R-2 (backward: its round 0 is peeled below)
-    const uint32_t tend = bwd ? R - 1 : R;
-    for (uint32_t t = 1; t < tend; t++) {
-        uint32_t w[kWords];
-#pragma unroll
-        for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-        if (t + 1 < R) {
-            const uint32_t kn = bwd ? R - 2 - t : t + 1;
-            if (bwd && kn == 0) load_unit0<false, false>(nxt, u0, fp, Lg, pad, dummy);
-            else load_ilv(nxt, span_lane + (uint64_t)kn * kStep, G);
-        }
-        ilv_to_units<GT>(w, g);
-        if ((bwd ? R - 1 - t : t) == 1u && seed_spill) w[0] ^= spill;
-        const uint32_t mp = map_apply(acc, bwd ? bmap : gmap);
-        uint32_t c = bwd ? 0u : mp;
-#pragma unroll
-        for (int i = 0; i < kWords; i++) c = s4_step(c, w[i], sb);
-        acc = bwd ? c ^ mp : c;
-    }
-    // backward lanes: round 0, the start of the frame (masked, seeded), then
-    // the register is advanced over the (R - 1) G 64 bytes after round 0
-    int first0 = (bwd && u0 >= 0) ? (u0 == 0 ? (int)(pad >> 2) : 0) : kWords;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) first0 = min(first0, __shfl_xor(first0, o));
-    first0 = __builtin_amdgcn_readfirstlane(first0);
-    if (bwd) {
-        uint32_t w[kWords];
-#pragma unroll
-        for (int i = 0; i < kWords; i++) w[i] = nxt[i];
-        if (u0 == 0 && Lg >= 4) unit0_line_shift(w, fp, pad);
-        unit0_finish(w, u0, Lg, pad, seed);
-        acc = s4_words_from(first0, w, sb) ^ map_apply(acc, bmap);
-        acc = shift_bytes(acc, (R - 1u) << (6 + lgG), p.consts);
-    }
-    uint32_t tail[3] = {0, 0, 0}, trailer = 0;
-    if (last_lane) {
-        if (bwd) {
-#pragma unroll
-            for (uint32_t j = 0; j < 3; j++) tail[j] = (e0 >> (8 * j)) & 0xFFu;
-            trailer = tb ? (e0 >> (8 * tb)) | (e1 << (32 - 8 * tb)) : e0;
-        } else {
-            if (tb && Lg >= 4) {
-#pragma unroll
-                for (uint32_t j = 0; j < 3; j++) tail[j] = fp[Lg + min(j, tb - 1)];
-            }
-            if (p.verify) trailer = ld32(fp + L);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxTree; j++) {
-        if ((1 << j) >= G) break;
-        const uint32_t other = __shfl_xor(acc, 1 << j);
-        const bool right = (g >> j) & 1;
-        const uint32_t left = right ? other : acc;
-        acc = map_apply(left, tree_map(j)) ^ (right ? acc : other);
-    }
-    if (last_lane) {
-        if (Lg >= 4) {
-#pragma unroll
-            for (uint32_t j = 0; j < 3; j++)
-                if (j < tb) acc = byte_step(acc, tail[j], sb);
-        }
-        const uint32_t crc = acc ^ p.xorout;
-        if (p.out_crc && !DEFER) p.out_crc[f] = crc;
-        if (p.verify) {
-            const bool good = (crc == trailer);
-            if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
-            if (!good && p.nbad) atomicAdd(p.nbad, 1u);
-        }
-    }
-    return acc;
-}
-
-// The frames kernels' per-group hash: bidirectional at G = 2 and 4 (PF = 1,
-// no payload states), else hash_frame.
-template <int G, int PF, bool PAY, bool C0, bool DEFER, typename Pre, typename Mid = NoMid>
-__device__ __forceinline__ uint32_t frame_hash(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
-                                           const SliceBases &sb, Pre &&pre, Mid &&mid = Mid{})
-{
-    if constexpr (bidir_frames<G, PF, PAY>())
-        return hash_frame_bd<G, C0, DEFER>(p, f, active, off, L, g, sb, pre, mid);
-    else
-        return hash_frame<G, PF, PAY, false, C0, DEFER>(p, f, active, off, L, g, sb, G, pre, mid);
 }
 
 #ifdef VCRC_TIMING  // diagnostic builds only (tools/timing_cfg2.py): per-wave s_memrealtime stamps
@@ -774,45 +580,15 @@ __device__ uint32_t g_vcrc_info[4096];  // ragged: class << 16 | (L >> 6) of lan
 // the static deal is kept.
 // One frame group of a uniform wave: hash group f.., fetch the next group's
 // descriptors meanwhile, advance.
-// Deferred trailer-CRC store (VCRC_DEFER_STORE, A/B): a group's CRCs are
-// stored once the next group's first loads are issued (in its pre() hook),
-// not between the group's last round and the next group's loads, so the next
-// group's first wait on the in-order vector-memory counter does not also
-// wait for the store to complete.
-#ifndef VCRC_DEFER_STORE
-#define VCRC_DEFER_STORE 0
-#endif
-struct PendingCrc {
-    uint64_t f = 0;
-    uint32_t crc = 0;
-    bool v = false;
-    __device__ __forceinline__ void flush(const FrameParams &p)
-    {
-        if (v && p.out_crc) p.out_crc[f] = crc;
-        v = false;
-    }
-    __device__ __forceinline__ void set(const FrameParams &p, uint64_t fr, bool lane_out, uint32_t acc)
-    {
-        v = lane_out;
-        f = fr;
-        crc = acc ^ p.xorout;
-    }
-};
-
 template <int G, int PF, bool PAY, bool C0, typename Pre>
 __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, uint64_t &off, uint32_t &L, uint64_t &fb,
-                                           uint64_t step, int lane, const SliceBases &sb, PendingCrc &pend, Pre &&pre)
+                                           uint64_t step, int lane, const SliceBases &sb, Pre &&pre)
 {
-    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
     const uint64_t fn = f + step;
     uint64_t off_n = 0;
     uint32_t L_n = 0;
     if (fn < p.n) frame_desc(p, fn, off_n, L_n);
-    const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(p, f, f < p.n, off, L, lane % G, sb, [&] {
-        pre();
-        if (DEF) pend.flush(p);
-    });
-    if (DEF) pend.set(p, f, f < p.n && lane % G == G - 1, acc);
+    hash_frame<G, PF, PAY, false, C0>(p, f, f < p.n, off, L, lane % G, sb, G, pre);
     f = fn;
     off = off_n;
     L = L_n;
@@ -833,8 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     LdsImage im;
     lds_tables_issue(p.consts, im);
     PowImage pim;
-    constexpr bool POW = PAY || bidir_frames<G, PF, PAY>();  // payload states, backward frames' final shift
-    if (POW) lds_pow_issue(p.consts, 0, pim);
+    if (PAY) lds_pow_issue(p.consts, 0, pim);
     // Descriptors of the next frame group are fetched while this one hashes.
     // (Loading the first group's descriptors branch-free before the blob, so
     // the prologue overlaps the first frame loads exactly, measured slower:
@@ -848,19 +623,16 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // loop.
     const LdsImage &cim = im;
     const PowImage &cpim = pim;
-    constexpr bool DEF = VCRC_DEFER_STORE && !PAY;
-    PendingCrc pend;
-    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [&cim, &cpim] {
+    group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
-        if (POW) lds_pow_write(cpim);
+        if (PAY) lds_pow_write(cpim);
         __syncthreads();
         VCRC_STAMP(1);
     });
     if (!p.qhead) {
-        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
-        if (DEF) pend.flush(p);
+        while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
         VCRC_STAMP(2);
         return;
     }
@@ -873,7 +645,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // groups keep one word, which evens the end out better. The last wave out
     // re-zeroes the heads for the next launch on this stream.
     const uint64_t dyn = (uint64_t)p.static_rounds * nwaves * kGroups;  // first frame of the queue
-    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, pend, [] {});
+    while (fb < p.n && fb < dyn) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
     const uint32_t P = min(min(p.qparts, kDynParts), gridDim.x), part = blockIdx.x % P;
     // the lane id again from mbcnt: kept live from the entry, it was the one
     // value k_frames<16/32, 1> spilled to scratch (a scratch kernel's waves
@@ -899,10 +671,7 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
             uint64_t od = 0;
             uint32_t Ld = 0;
             if (fd < p.n) frame_desc(p, fd, od, Ld);
-            const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(p, fd, fd < p.n, od, Ld, ql % G, sb, [&] {
-                if (DEF) pend.flush(p);
-            });
-            if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
+            hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {});
         }
     }
     uint32_t k = 0;
@@ -916,23 +685,16 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
         if (ql == 0) kn = atomicAdd(&p.qhead[part * 16u], 1u);
         uint64_t gb_n = 0, fd_n = 0, od_n = 0;
         uint32_t Ld_n = 0;
-        const uint32_t acc = frame_hash<G, PF, PAY, C0, DEF>(
-            p, fd, fd < p.n, od, Ld, ql % G, sb,
-            [&] {
-                if (DEF) pend.flush(p);
-            },
-            [&] {
-                gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
-                fd_n = gb_n + (uint64_t)(ql / G);
-                if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
-            });
-        if (DEF) pend.set(p, fd, fd < p.n && ql % G == G - 1, acc);
+        hash_frame<G, PF, PAY, false, C0>(p, fd, fd < p.n, od, Ld, ql % G, sb, G, [] {}, [&] {
+            gb_n = dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(kn)) * kGroups;
+            fd_n = gb_n + (uint64_t)(ql / G);
+            if (fd_n < p.n) frame_desc(p, fd_n, od_n, Ld_n);
+        });
         gb = gb_n;
         fd = fd_n;
         od = od_n;
         Ld = Ld_n;
     }
-    if (DEF) pend.flush(p);
     VCRC_STAMP(2);
     if (ql == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
