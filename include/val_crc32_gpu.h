@@ -272,9 +272,12 @@ uint32_t val_gpu_lanes_per_frame(uint32_t typical_len);
  * process; 0 restores the automatic choice. Returns VAL_ERR_INVALID_ARG for
  * other values. Results never depend on it; only speed does. */
 val_status_t val_gpu_set_lanes_per_frame(uint32_t lanes);
-/* Rounds of each lane's input kept in flight ahead of the one being hashed
- * (0, 1, 2 or 4; -1 = automatic: 1 for multi-pass batches, deeper when a batch
- * fits in one pass of the grid). Speed only; results never change. */
+/* Rounds of each lane's input kept in flight ahead of the one being hashed:
+ * 0, 1, 2 or 4 (copy and refill), or -2 / -3 (a ring of 2 or 3 rounds hashed
+ * in their registers and refilled in place; 2 and 4 lanes per frame only,
+ * others run 1); -1 = automatic: the 3-ring at 2 lanes, the 2-ring at 4 lanes
+ * for frames under 1,600 B,
+ * 1 otherwise. Speed only; results never change. */
 val_status_t val_gpu_set_prefetch(int depth);
 /* Mixed-length descriptor batches (len_hint 0) of at least this many frames
  * are binned by length on the device; smaller ones run uniform. -1 restores

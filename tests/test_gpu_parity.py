@@ -11,8 +11,9 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 GEOMS = [1, 2, 4, 8, 16, 32, 64]
-# register prefetch depths of the frames kernel (0 = off)
-VARIANTS = [(0,), (1,), (2,), (4,)]
+# register prefetch depths of the frames kernel (0 = off; -2, -3: in-place
+# rings, G = 2 and 4)
+VARIANTS = [(0,), (1,), (2,), (4,), (-2,), (-3,)]
 
 
 @pytest.fixture(scope="module")
@@ -571,3 +572,32 @@ def test_dynamic_tail_every_frame(vc, dev, strided, payload, per):
         crc = vc.frames(buf, **kw)
         torch.cuda.synchronize()
         assert np.array_equal(_u32(crc), want)
+
+
+@pytest.mark.parametrize("G,depth", [(2, -1), (4, -1), (2, -2), (4, -3), (2, 1), (4, 1)])
+def test_ring_prefetch_multi_pass(vc, dev, G, depth):
+    """Multi-pass batches at 2 and 4 lanes per frame hash each round in its
+    registers and refill them in place (rings of 3 and 2 rounds by default):
+    mixed lengths 0..3,000 B (1 to 24 rounds, so frames longer than the ring
+    refill it), unaligned starts, against the oracle, with the automatic depth
+    (-1), the other ring, and the copy-and-refill loop."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 16 * (64 // G) * 3 + 555  # three passes of the machine and a partial one
+    base, offs, lens = _ragged_fast(0x71 + G, n, 0, 3000)
+    vc.set_geometry(G, depth)
+    try:
+        d = torch.from_numpy(base).to(dev)
+        crc = vc.frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
+                        length=torch.from_numpy(lens.view(np.int32)).to(dev), len_hint=1500)
+        torch.cuda.synchronize()
+    finally:
+        vc.set_geometry()
+    assert np.array_equal(_u32(crc), _oracle.frames(base, offs, lens, nthreads=16))
+
+
+def _ragged_fast(seed, n, lo, hi):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offs = np.cumsum(lens.astype(np.uint64) + 4 + rng.integers(0, 7, n).astype(np.uint64)) - lens - 4
+    base = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 16, dtype=np.uint8)
+    return base, offs.astype(np.uint64), lens

@@ -367,7 +367,11 @@ template <int GT, int PF, bool PAY, bool BF, bool C0 = false, typename Pre, type
 __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f, bool active, uint64_t off, uint32_t L, int g,
                                            const SliceBases &sb, int Gr, Pre &&pre, Mid &&mid = Mid{})
 {
-    constexpr int D = PF > 0 ? PF : 1;
+    // PF < 0 (burst): rounds 1..-PF are all issued with round 0 and hashed in
+    // place, never refilled; rounds past them (frames longer than the burst)
+    // are loaded one at a time after it.
+    constexpr bool BURST = PF < 0;
+    constexpr int D = PF > 0 ? PF : (BURST ? -PF : 1);
     const int G = GT ? GT : Gr;
     const uint32_t gmap = gap_map(GT ? ilog2(GT) : __builtin_ctz((unsigned)Gr));
     gu8 *fp = gptr(p.base) + off;
@@ -402,7 +406,7 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     constexpr bool ILV = ilv_lanes<GT>() && !BF && !C0;
     gu8 *const ilv_up = up - 48 * g;  // round 1's span + 16 g (ILV)
     uint32_t nxt[D][kWords];
-    if (PF > 0) {
+    if (PF != 0) {
 #pragma unroll
         for (int d = 0; d < D; d++) {
             if (ILV) {
@@ -459,6 +463,27 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
             if (G > 1) acc = map_apply(acc, gmap);
 #pragma unroll
             for (int i = 0; i < kWords; i++) acc = s4_step(acc, w[i], sb);
+        }
+    } else if (BURST) {
+        // ring in place: round k sits in nxt[(k - 1) % D], is hashed there, and
+        // its registers are then refilled with round k + D (no copy, so the
+        // D - 1 rounds after it stay in flight while it is hashed)
+        for (uint32_t k = 1; k < R; k += D) {
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const uint32_t kk = k + d;
+                if (kk < R) {
+                    if (ILV) ilv_to_units<GT>(nxt[d], g);
+                    if (kk == 1 && seed_spill) nxt[d][0] ^= seed >> (8 * (kUnit - pad));
+                    if (G > 1) acc = map_apply(acc, gmap);
+#pragma unroll
+                    for (int i = 0; i < kWords; i++) acc = s4_step(acc, nxt[d][i], sb);
+                    if (kk + D < R) {
+                        if (ILV) load_ilv(nxt[d], ilv_up + (uint64_t)(kk + D - 1) * kStep, G);
+                        else load_full(nxt[d], up + (uint64_t)(kk + D - 1) * kStep);
+                    }
+                }
+            }
         }
     } else {
         // nxt[d] holds round k + d; once consumed it is refilled with round k + d + D.

@@ -297,25 +297,27 @@ uint32_t lanes_for_batch(const Ctx &c, uint32_t len, uint64_t n)
     return G;
 }
 
-bool valid_prefetch(int d) { return d == 0 || d == 1 || d == 2 || d == 4; }
+// 0, 1, 2, 4: copy-and-refill depths; -2, -3: in-place rings (G = 2 and 4 only)
+bool valid_prefetch(int d) { return d == 0 || d == 1 || d == 2 || d == 4 || d == -2 || d == -3; }
 
 // Prefetch depth forced by val_gpu_set_prefetch or VAL_GPU_PREFETCH (-1 = none).
 int forced_prefetch()
 {
     static const int env_p = getenv("VAL_GPU_PREFETCH") ? atoi(getenv("VAL_GPU_PREFETCH")) : -1;
     const int forced = g_forced_prefetch.load(std::memory_order_relaxed);
-    if (forced >= 0) return forced;
+    if (forced != -1) return forced;
     return valid_prefetch(env_p) ? env_p : -1;
 }
 
-// Rounds kept in flight ahead of the one being hashed: 1 unless forced.
+// Rounds kept in flight ahead of the one being hashed: 1 unless forced
+// (launch_uniform_g turns the automatic 1 into the in-place rings at G = 2, 4).
 // Measured on MI355X (profiles/r01_small_batches.log): issuing every round up
 // front (2 or 4 deep) lost 5-15% even on one-pass batches such as cfg2, since
 // the whole batch's requests then land before any wave can start hashing.
 int prefetch_depth()
 {
     const int forced = forced_prefetch();
-    return forced >= 0 ? forced : 1;
+    return forced != -1 ? forced : 1;
 }
 
 StreamScratch &scratch_for(Ctx &c, hipStream_t s);
@@ -326,11 +328,29 @@ hipError_t launch_tracked(StreamScratch *x, K kernel, dim3 grid, dim3 block, hip
 // 0's units by dword loads (k_frames C0; crc_kernels.hpp load_unit0).
 // x: the stream scratch the launch uses (the dynamic-tail queue), else null.
 template <int G>
-hipError_t launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p, bool one_pass, StreamScratch *x)
+hipError_t launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams &p, bool one_pass, StreamScratch *x,
+                             uint32_t len)
 {
     const dim3 b(kBlock);
     if (p.out_pay) return launch_tracked(x, k_frames<G, 1, true>, grid, b, s, p);  // payload states: default depth only
     if (pf == 1 && one_pass) return launch_tracked(x, k_frames<G, 1, false, true>, grid, b, s, p);
+    // Multi-pass short frames hash each round in its registers and refill them
+    // in place (a ring of -pf rounds, crc_kernels.hpp hash_frame BURST):
+    // profiles/r04_ab_ring_prefetch.log, same box against the copy-and-refill
+    // PF = 1 loop: G = 2 three deep u600d +4.2% (two deep +1.8%); G = 4 two
+    // deep u1100d +1.5-1.8%, s1100 0%, u2000d -0.3 to -0.6% (three deep -0.7 to
+    // -3%), so 4 lanes take the ring below 1,600 B (R <= 7) only.
+#ifndef VCRC_RING_G2
+#define VCRC_RING_G2 -3
+#endif
+#ifndef VCRC_RING_G4
+#define VCRC_RING_G4 -2
+#endif
+    if (pf == 1 && forced_prefetch() == -1) pf = G == 2 ? VCRC_RING_G2 : (G == 4 && len < 1600u) ? VCRC_RING_G4 : 1;
+    if constexpr (G == 2 || G == 4) {
+        if (pf == -3) return launch_tracked(x, k_frames<G, -3, false>, grid, b, s, p);
+        if (pf == -2) return launch_tracked(x, k_frames<G, -2, false>, grid, b, s, p);
+    }
     switch (pf) {
     case 0: return launch_tracked(x, k_frames<G, 0, false>, grid, b, s, p);
     case 2: return launch_tracked(x, k_frames<G, 2, false>, grid, b, s, p);
@@ -375,7 +395,7 @@ bool split_enabled()
 
 bool use_split(const Ctx &c, const FrameParams &p, uint32_t len)
 {
-    if (!split_enabled() || p.out_pay || forced_lanes() || forced_prefetch() >= 0 || len < 8192u) return false;
+    if (!split_enabled() || p.out_pay || forced_lanes() || forced_prefetch() != -1 || len < 8192u) return false;
     const uint64_t waves = (uint64_t)c.cus * kWavesPerBlock;
     if ((uint64_t)p.n * 2u > waves) return false;
     const uint64_t rounds = ((uint64_t)len / kUnit + 1u + 63u) / 64u;  // at one wave per frame
@@ -454,13 +474,13 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     const bool one_pass = ((uint64_t)p.n + 64 / G - 1) / (64 / G) <= (uint64_t)grid.x * kWavesPerBlock;
     hipError_t e = hipSuccess;
     switch (G) {
-    case 1: e = launch_uniform_g<1>(pf, grid, s, p, one_pass, used); break;
-    case 2: e = launch_uniform_g<2>(pf, grid, s, p, one_pass, used); break;
-    case 4: e = launch_uniform_g<4>(pf, grid, s, p, one_pass, used); break;
-    case 8: e = launch_uniform_g<8>(pf, grid, s, p, one_pass, used); break;
-    case 16: e = launch_uniform_g<16>(pf, grid, s, p, one_pass, used); break;
-    case 32: e = launch_uniform_g<32>(pf, grid, s, p, one_pass, used); break;
-    case 64: e = launch_uniform_g<64>(pf, grid, s, p, one_pass, used); break;
+    case 1: e = launch_uniform_g<1>(pf, grid, s, p, one_pass, used, len); break;
+    case 2: e = launch_uniform_g<2>(pf, grid, s, p, one_pass, used, len); break;
+    case 4: e = launch_uniform_g<4>(pf, grid, s, p, one_pass, used, len); break;
+    case 8: e = launch_uniform_g<8>(pf, grid, s, p, one_pass, used, len); break;
+    case 16: e = launch_uniform_g<16>(pf, grid, s, p, one_pass, used, len); break;
+    case 32: e = launch_uniform_g<32>(pf, grid, s, p, one_pass, used, len); break;
+    case 64: e = launch_uniform_g<64>(pf, grid, s, p, one_pass, used, len); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
     VCRC_HIP(e, "k_frames launch");
@@ -1728,8 +1748,9 @@ void val_gpu_host_free(void *p)
 
 val_status_t val_gpu_set_prefetch(int depth)
 {
-    if (depth >= 0 && !valid_prefetch(depth)) return fail(VAL_ERR_INVALID_ARG, "prefetch depth must be -1, 0, 1, 2 or 4");
-    g_forced_prefetch.store(depth < 0 ? -1 : depth, std::memory_order_relaxed);
+    if (depth != -1 && !valid_prefetch(depth))
+        return fail(VAL_ERR_INVALID_ARG, "prefetch depth must be -1, 0, 1, 2, 4, -2 or -3");
+    g_forced_prefetch.store(depth, std::memory_order_relaxed);
     return VAL_OK;
 }
 
