@@ -333,7 +333,13 @@ hipError_t launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams 
 {
     const dim3 b(kBlock);
     if (p.out_pay) return launch_tracked(x, k_frames<G, 1, true>, grid, b, s, p);  // payload states: default depth only
-    if (pf == 1 && one_pass) return launch_tracked(x, k_frames<G, 1, false, true>, grid, b, s, p);
+// A/B builds: one-pass launches' round loop. Rings measured no better on
+// cfg2 (two deep +0.6% back to back, -3.7% single launch; three deep -7%) and
+// equal on 64-4,096-frame windows (profiles/r04_ab_ring_prefetch_one_pass.log).
+#ifndef VCRC_C0_PF
+#define VCRC_C0_PF 1
+#endif
+    if (pf == 1 && one_pass) return launch_tracked(x, k_frames<G, (G == 2 || G == 4) ? VCRC_C0_PF : 1, false, true>, grid, b, s, p);
     // Multi-pass short frames hash each round in its registers and refill them
     // in place (a ring of -pf rounds, crc_kernels.hpp hash_frame BURST):
     // profiles/r04_ab_ring_prefetch.log, same box against the copy-and-refill
@@ -672,7 +678,13 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
         // the ragged kernel is the last of the three on the stream to use the scratch
         if (p.out_pay) e = launch_tracked(&ss, k_frames_ragged<1, true>, dim3(blocks), dim3(kBlock), s, p);
         else if (forced_prefetch() == 0) e = launch_tracked(&ss, k_frames_ragged<0, false>, dim3(blocks), dim3(kBlock), s, p);
-        else e = launch_tracked(&ss, k_frames_ragged<1, false>, dim3(blocks), dim3(kBlock), s, p);
+// A/B builds: the ragged kernel's round loop (1 = copy and refill, -2 / -3 =
+// rings). The rings lost 9-11% on cfg5 and the class-2 mix and 2-3% on 600 and
+// 1,100-B frames through the ragged path (profiles/r04_ab_ring_prefetch_ragged.log).
+#ifndef VCRC_RAGGED_PF
+#define VCRC_RAGGED_PF 1
+#endif
+        else e = launch_tracked(&ss, k_frames_ragged<VCRC_RAGGED_PF, false>, dim3(blocks), dim3(kBlock), s, p);
         a.counts_zero = e == hipSuccess;
     }
     if (e != hipSuccess) return fail(VAL_ERR_IO, "ragged frames launch", e);
