@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--sort-frames", action="store_true", help="cfg5: order descriptors by length (diagnostic)")
     ap.add_argument("--no-cfg4-strong", action="store_true",
                     help="skip the cfg4 strong-scaling block (BASELINE configs[3]) timed after the headline")
+    ap.add_argument("--with-cfg4-strong", action="store_true",
+                    help="also time the cfg4 strong-scaling block after a weak config other than cfg3 "
+                         "(by default only the cfg3 headline line carries it)")
     return ap.parse_args()
 
 
@@ -555,7 +558,8 @@ def main():
     # 65,536 sharded over the ranks by val_shard_frames (strong scaling),
     # timed like the headline, its own per-rank records and aggregate.
     strong_block = None
-    if not strong and not args.no_cfg4_strong and not args.verify and not args.sort_frames:
+    want_strong = (args.config == "cfg3" or args.with_cfg4_strong) and not args.no_cfg4_strong
+    if want_strong and not strong and not args.verify and not args.sort_frames:
         del flats, flat, buf, w, crc, hdr, ok, pay, kw
         torch.cuda.empty_cache()
         w4 = build_workload(torch, dev, "cfg4", rank, world, False, vc)

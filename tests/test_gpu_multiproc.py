@@ -30,11 +30,11 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _bench_two_ranks(config: str) -> dict:
+def _bench_two_ranks(config: str, *extra: str) -> dict:
     env = dict(os.environ, VAL_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+           "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline", *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -43,7 +43,8 @@ def _bench_two_ranks(config: str) -> dict:
 
 
 def test_bench_two_ranks_weak_cfg2():
-    line = _bench_two_ranks("cfg2")
+    # (the cfg3 headline carries the cfg4 block by default; cfg2 asks for it, to stay small)
+    line = _bench_two_ranks("cfg2", "--with-cfg4-strong")
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["parity_sample_ok"] is True
     assert line["config"]["frames_per_gpu"] == 65536

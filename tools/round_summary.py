@@ -47,7 +47,7 @@ def traffic(o, fetch, write, cfg, out_name):
     return d
 
 
-def kernel_trace(o, sub, rnd, tag):
+def kernel_trace(o, sub, rnd, tag, prefer=None):
     d = os.path.join(o, sub)
     stats = os.path.join(d, "bench_kernel_stats.csv")
     if not os.path.exists(stats):
@@ -60,7 +60,9 @@ def kernel_trace(o, sub, rnd, tag):
         w.writerow(["Dispatch_Id", "Kernel_Name", "duration_ns"])
         for r in crc:
             w.writerow([r["Dispatch_Id"], r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"])])
-    top = max(csv.DictReader(open(stats)), key=lambda r: float(r["TotalDurationNs"]))
+    kstats = list(csv.DictReader(open(stats)))
+    pick = [r for r in kstats if prefer and prefer in r["Name"]] or kstats  # the config's own kernel first
+    top = max(pick, key=lambda r: float(r["TotalDurationNs"]))
     main = [r for r in crc if r["Kernel_Name"] == top["Name"]]
     steps = int(os.environ.get("BENCH_STEPS", "20"))  # bench.py's timed steps (default 20, after 15 warmup)
     extra = min(steps, 5)  # bench.py's untimed per-step pass after the timed region (round 3 on)
@@ -79,7 +81,7 @@ def main():
     s["other_bench_lines"] = [b for b in (bench_line(os.path.join(o, f"bench_{k}.json"))
                                           for k in ("verify", "cfg4", "cfg2", "cfg5")) if b]
     s["rocprof_cfg3"] = kernel_trace(o, "trace", rnd, "cfg3")
-    s["rocprof_cfg5"] = kernel_trace(o, "trace5", rnd, "cfg5")
+    s["rocprof_cfg5"] = kernel_trace(o, "trace5", rnd, "cfg5", prefer="k_frames_ragged")
     s["pmc_traffic_cfg3"] = traffic(o, "pmc_fetch", "pmc_write", "cfg3", "pmc_cfg3.json")
     s["pmc_traffic_cfg3_verify"] = traffic(o, "pmc_fetch_v", None, "cfg3_verify", "pmc_cfg3_verify.json")
     s["pmc_traffic_cfg5"] = traffic(o, "pmc_fetch5", "pmc_write5", "cfg5", "pmc_cfg5.json")
