@@ -152,38 +152,45 @@ constexpr uint32_t kConstWords = kConstPowHi + 16;
 // runs under the LDS fill and the barrier instead of after them (with no
 // LDS-DMA in flight, __syncthreads() is a bare s_barrier: plain loads stay
 // outstanding across it).
-struct LdsImage {
-    uint32_t v[8], vm[2];
+// NT = threads of the workgroup that fills the tables (1,024, or 512 for the
+// eight-wave short-frame kernels): each thread holds 8192 / NT table chunks and
+// 2048 / NT map words.
+template <int NT = kBlock>
+struct LdsImageT {
+    uint32_t v[8 * kBlock / NT], vm[2 * kBlock / NT];
 };
+using LdsImage = LdsImageT<kBlock>;
 
-__device__ __forceinline__ void lds_tables_issue(const uint32_t *consts, LdsImage &im)
+template <int NT>
+__device__ __forceinline__ void lds_tables_issue(const uint32_t *consts, LdsImageT<NT> &im)
 {
     const uint32_t t = threadIdx.x;
     constexpr uint32_t kMapWords = kNumMaps * 128u;
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const uint32_t c = (uint32_t)r * kBlock + t, row = c >> 4;
+    for (int r = 0; r < 8 * kBlock / NT; r++) {
+        const uint32_t c = (uint32_t)r * NT + t, row = c >> 4;
         const uint32_t slot = (row >> 8) * 2u + ((c >> 3) & 1u);
         im.v[r] = consts[kConstSlice + (3u - slot) * 256u + (row & 255u)];
     }
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const uint32_t i = (uint32_t)r * kBlock + t;
+    for (int r = 0; r < 2 * kBlock / NT; r++) {
+        const uint32_t i = (uint32_t)r * NT + t;
         im.vm[r] = i < kMapWords ? consts[kConstGap + i] : 0u;
     }
 }
 
-__device__ __forceinline__ void lds_tables_write(const LdsImage &im)
+template <int NT>
+__device__ __forceinline__ void lds_tables_write(const LdsImageT<NT> &im)
 {
     const uint32_t t = threadIdx.x;
     constexpr uint32_t kMapWords = kNumMaps * 128u;
     uint4 *lds4 = reinterpret_cast<uint4 *>(s_lds);
 #pragma unroll
-    for (int r = 0; r < 8; r++)
-        lds4[(kLdsS4 / 16u) + (uint32_t)r * kBlock + t] = make_uint4(im.v[r], im.v[r], im.v[r], im.v[r]);
+    for (int r = 0; r < 8 * kBlock / NT; r++)
+        lds4[(kLdsS4 / 16u) + (uint32_t)r * NT + t] = make_uint4(im.v[r], im.v[r], im.v[r], im.v[r]);
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const uint32_t i = (uint32_t)r * kBlock + t;
+    for (int r = 0; r < 2 * kBlock / NT; r++) {
+        const uint32_t i = (uint32_t)r * NT + t;
         if (i < kMapWords) s_lds[kLdsMaps / 4u + i] = im.vm[r];
     }
 }

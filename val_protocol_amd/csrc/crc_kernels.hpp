@@ -620,8 +620,11 @@ __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, ui
     fb += step;
 }
 
-template <int G, int PF, bool PAY, bool C0 = false>
-__global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
+// BT: threads per workgroup. 1,024 (16 waves, 128 VGPRs) everywhere, or 512
+// (8 waves, up to 256 VGPRs: deeper rings for short frames; an A/B that lost
+// 10-24%, val_crc32_hip.hip VCRC_W8_PF).
+template <int G, int PF, bool PAY, bool C0 = false, int BT = kBlock>
+__global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
 {
     VCRC_STAMP(0);
     VCRC_KARG_EARLY("s"(p.consts), "s"(p.base), "s"(p.off), "s"(p.len), "s"(p.stride), "s"(p.flen), "s"(p.last_len),
@@ -629,12 +632,13 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     constexpr int kGroups = 64 / G;
     const int lane = threadIdx.x & 63;
     const SliceBases sb = slice_bases((uint32_t)(lane & 31) << 2);
-    const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
-    LdsImage im;
+    static_assert(BT == kBlock || !PAY, "payload states need the 1,024-thread pow-map fill");
+    const uint64_t wave = ((uint64_t)blockIdx.x * BT + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * BT) >> 6;
+    LdsImageT<BT> im;
     lds_tables_issue(p.consts, im);
     PowImage pim;
-    if (PAY) lds_pow_issue(p.consts, 0, pim);
+    if constexpr (PAY) lds_pow_issue(p.consts, 0, pim);
     // Descriptors of the next frame group are fetched while this one hashes.
     // (Loading the first group's descriptors branch-free before the blob, so
     // the prologue overlaps the first frame loads exactly, measured slower:
@@ -646,13 +650,13 @@ __global__ __launch_bounds__(kBlock) void k_frames(const FrameParams p)
     // LDS fill and the barrier sit in its hash_frame call, after the frame
     // loads are issued. Peeled, so the LDS image's registers are dead in the
     // loop.
-    const LdsImage &cim = im;
+    const LdsImageT<BT> &cim = im;
     const PowImage &cpim = pim;
     group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [&cim, &cpim] {
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
-        if (PAY) lds_pow_write(cpim);
+        if constexpr (PAY) lds_pow_write(cpim);
         __syncthreads();
         VCRC_STAMP(1);
     });

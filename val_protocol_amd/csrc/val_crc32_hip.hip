@@ -424,7 +424,18 @@ val_status_t launch_split(const Ctx &c, FrameParams &p, uint32_t len, hipStream_
 val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32_t len, hipStream_t s)
 {
     p.consts = c.d_consts;
-    const uint64_t groups_per_block = (uint64_t)kWavesPerBlock * (64 / G);
+// A/B builds: multi-pass G = 2/4 batches on 512-thread workgroups (8 waves
+// per CU, up to 256 VGPRs: 185 used) with a ring of -VCRC_W8_PF rounds, so a
+// 1,100-B group's rounds are all in flight at entry. 10-24% slower than 16
+// waves with the 2/3-rings (u1100d -23%, s1100 -18%, u600d -11%, u2000d -10%;
+// profiles/r04_ab_eight_waves_deep_ring.log): the table chains need the waves.
+#ifndef VCRC_W8_PF
+#define VCRC_W8_PF 0
+#endif
+    const bool w8 = VCRC_W8_PF != 0 && (G == 2 || G == 4) && !p.out_pay && forced_prefetch() == -1 &&
+                    (uint64_t)p.n > (uint64_t)c.cus * 16u * (64u / G);  // more than one pass at 16 waves per CU
+    const uint32_t wpb = w8 ? 8u : (uint32_t)kWavesPerBlock;
+    const uint64_t groups_per_block = (uint64_t)wpb * (64 / G);
     uint64_t blocks = (p.n + groups_per_block - 1) / groups_per_block;
     blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)c.cus));  // persistent, 1 per CU (LDS)
     const dim3 grid((unsigned)blocks);
@@ -439,7 +450,7 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     // strided ones from 32 KiB (s4200 +3%; s1100's 17.6 KiB groups -3%);
     // descriptor groups of 128-192 KiB stay static (u16400d -1% either way):
     // profiles/r02_ab_dynparts.log.
-    const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * kWavesPerBlock);
+    const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * wpb);
     p.qhead = nullptr;
     const uint64_t group_bytes = (uint64_t)(64 / G) * len;
 #ifndef VCRC_DYN_MIN_GROUP  // A/B builds may override: one-word minimum group bytes, strided / descriptor batches
@@ -477,8 +488,14 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
 #endif
         p.static_rounds = (uint32_t)(VCRC_DYN_DIV == 1 ? 1u : rounds - std::max<uint64_t>(1, rounds / VCRC_DYN_DIV));
     }
-    const bool one_pass = ((uint64_t)p.n + 64 / G - 1) / (64 / G) <= (uint64_t)grid.x * kWavesPerBlock;
+    const bool one_pass = ((uint64_t)p.n + 64 / G - 1) / (64 / G) <= (uint64_t)grid.x * wpb;
     hipError_t e = hipSuccess;
+    if (w8) {
+        if (G == 2) e = launch_tracked(used, k_frames<2, (VCRC_W8_PF < 0 ? VCRC_W8_PF : -2), false, false, 512>, grid, dim3(512), s, p);
+        else e = launch_tracked(used, k_frames<4, (VCRC_W8_PF < 0 ? VCRC_W8_PF : -2), false, false, 512>, grid, dim3(512), s, p);
+        VCRC_HIP(e, "k_frames launch");
+        return VAL_OK;
+    }
     switch (G) {
     case 1: e = launch_uniform_g<1>(pf, grid, s, p, one_pass, used, len); break;
     case 2: e = launch_uniform_g<2>(pf, grid, s, p, one_pass, used, len); break;
