@@ -656,7 +656,7 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
 #ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the prologue's share of small launches
         lds_tables_write(cim);
 #endif
-        if constexpr (PAY) lds_pow_write(cpim);
+        if (PAY) lds_pow_write(cpim);
         __syncthreads();
         VCRC_STAMP(1);
     });
