@@ -314,7 +314,7 @@ def timed_steps(torch, dist, world, step, steps, warmup, stream):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -324,7 +324,7 @@ def timed_steps(torch, dist, world, step, steps, warmup, stream):
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
@@ -332,7 +332,7 @@ def timed_steps(torch, dist, world, step, steps, warmup, stream):
 
 def max_over_ranks(torch, dist, world, value, dev, backend):
     t = torch.tensor([value], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -371,7 +371,7 @@ def rank_record(w, rank, gpu, steps, elapsed, kern_ms, parity):
 
 
 def gather(dist, world, mine):
-    if world == 1:
+    if not dist.is_initialized():
         return [mine]
     out = [None] * world
     dist.all_gather_object(out, mine)
@@ -446,7 +446,9 @@ def main():
               file=sys.stderr, flush=True)
         sys.exit(2)
     gpu = local % max(ndev, 1)  # == local on a full node; with gloo a 1-GPU box rehearses N ranks
-    if world > 1:
+    # VAL_BENCH_FORCE_DIST=1: a process group even for one rank (the RCCL path
+    # on a one-GPU box: init, barriers, all_reduce, all_gather_object)
+    if world > 1 or os.environ.get("VAL_BENCH_FORCE_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(gpu)
         if backend == "nccl":
@@ -641,7 +643,7 @@ def main():
             **({"cfg4_strong": strong_block} if strong_block is not None else {}),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -8,6 +8,7 @@ gloo for the host-side collectives), with every CRC computed by the product:
     product's val_shard_region rule), each rank's partial register computed by
     val_crc32_region_dev on the GPU, gathered over gloo and folded with the
     product's val_crc32_fold_partials, against the oracle.
+And bench.py's RCCL path (nccl backend) with one rank on the box's GPU.
 SURVEY 8(e); reference window fill src/val_sender.c:822-841."""
 import json
 import os
@@ -67,6 +68,28 @@ def test_bench_two_ranks_weak_cfg2():
     file_crc_input = 131112 * (8 + 8 + 65516) + 8 + 8 + 800
     assert st["aggregate_over_max_rank"]["total_bytes"] == 2 * file_crc_input  # 2 steps
     assert st["value"] > 0
+
+
+def test_bench_rccl_process_group_one_rank():
+    """The RCCL (nccl backend) code path of bench.py on real hardware: one rank
+    under torch.distributed.run with a process group forced on, so the nccl
+    init with device_id, the barriers around the timed region, the GPU-tensor
+    all_reduce(MAX) and all_gather_object run through RCCL exactly as on the
+    driver's 8-GPU node (where each rank has its own GPU)."""
+    env = dict(os.environ, VAL_BENCH_BACKEND="nccl", VAL_BENCH_FORCE_DIST="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--config", "cfg2", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+           "--with-cfg4-strong"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["config"]["parity_sample_ok"] is True and line["value"] > 0
+    assert [x["rank"] for x in line["per_rank"]] == [0]
+    st = line["cfg4_strong"]
+    assert st["parity_sample_ok"] is True and st["per_rank"][0]["frames"] == 131113
 
 
 def test_bench_two_ranks_strong_cfg4():
