@@ -54,6 +54,10 @@ def workload(name, dev):
         lens = rng.integers(520, 65533, 262144)
     elif name == "u57":
         lens = np.full(56508, 57000)
+    elif name in ("c2h", "c2s"):  # c2's lengths through the uniform kernels (len_hint 16384), or sorted in memory
+        lens = np.exp(rng.uniform(np.log(8192), np.log(49151), 150000)).astype(np.int64)
+        if name == "c2s":
+            lens = np.sort(lens)[::-1].copy()
     elif name in ("c2", "c2a", "c2b", "c2d"):  # class-2 log-uniform mix, variants by alignment:
         # c2a: L = 12 mod 16 (frame starts 16-B aligned, units 12 mod 16, no tail bytes);
         # c2b: L = 0 mod 4 (no tail bytes, units at random 16-B phase);
@@ -73,7 +77,7 @@ def workload(name, dev):
     buf = torch.randint(0, 256, (int(wire.sum()) + 4,), dtype=torch.uint8, device=dev, generator=g)
     return dict(buf=buf, off=torch.from_numpy(off.astype(np.int64)).to(dev),
                 length=torch.from_numpy(lens.astype(np.int32)).to(dev),
-                len_hint=int(lens[0]) if name.endswith("d") else 0), int(lens.sum())
+                len_hint=16384 if name == "c2h" else int(lens[0]) if name.endswith("d") else 0), int(lens.sum())
 
 
 def main():

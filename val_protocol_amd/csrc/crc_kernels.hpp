@@ -511,6 +511,9 @@ __device__ __forceinline__ uint32_t hash_frame(const FrameParams &p, uint64_t f,
     // The tb <= 3 bytes past the grid and, on verify, the stored trailer: all
     // issued before the merge, which hides their round trip (a byte loop after
     // it waited once per byte).
+    // (One dword-aligned load for the tail bytes instead of three byte loads
+    // measured the same: cfg5 -0.2%, 1,101-B frames +0.2%;
+    // profiles/r04_ab_tail_dword.log.)
     uint32_t tail[3] = {0, 0, 0}, trailer = 0, pw[4] = {0, 0, 0, 0};
     if (active && g == G - 1) {
         if (tb && Lg >= 4) {
@@ -985,6 +988,10 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
         bool active_n = false;
         const int G = class_lanes(cur.c);
         VCRC_LAST_ITEM(cur.c, L);
+        // (One compile-time-G hash_frame instance per class instead, switched per
+        // item, spilled 6-8 VGPRs and ran 1.5-16% slower: cfg5 -1.5%, class-2 mix
+        // -2.4%, 1,100-B frames -16%; with the unit loads -0.3 to -7%;
+        // profiles/r04_ab_ragged_compile_time_lanes.log.)
         hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {}, [&] {
             it_n = part + P * (__builtin_amdgcn_readfirstlane(k_n) + nwp);
             if (it_n < items) {
