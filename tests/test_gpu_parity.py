@@ -595,6 +595,45 @@ def test_ring_prefetch_multi_pass(vc, dev, G, depth):
     assert np.array_equal(_u32(crc), _oracle.frames(base, offs, lens, nthreads=16))
 
 
+@pytest.mark.parametrize("G,depth", [(2, -1), (4, -1), (2, -2), (4, -3)])
+def test_ring_prefetch_verify_and_header(vc, dev, G, depth):
+    """The in-place rings on the verify kernel with header_crc (multi-pass):
+    trailers written by the oracle, 97 frames corrupted (trailer bytes and
+    frame bytes in every round position), verdicts, mismatch count, the
+    computed CRCs and header_crcs against the oracle."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 16 * (64 // G) * 2 + 333
+    base, offs, lens = _ragged_fast(0x91 + G, n, 8, 2500)
+    crc_want, hdr_want = _oracle.frames(base, offs, lens, header=True, nthreads=16)
+    tr = np.frombuffer(crc_want.astype("<u4").tobytes(), np.uint8).reshape(-1, 4)
+    idx = (offs + lens.astype(np.uint64)).astype(np.int64)
+    for k in range(4):
+        base[idx + k] = tr[:, k]
+    rng = np.random.default_rng(G)
+    bad = rng.choice(n, 97, replace=False)
+    for k, i in enumerate(bad):
+        o, l = int(offs[i]), int(lens[i])
+        pos = o + l + (k % 4) if k % 3 == 0 else o + int(rng.integers(0, l))
+        base[pos] ^= np.uint8(1 << (k % 8))
+    want_ok, want_bad = _oracle.verify_frames(base, offs, lens, nthreads=16)
+    assert want_bad == 97
+    vc.set_geometry(G, depth)
+    try:
+        d = torch.from_numpy(base).to(dev)
+        crc = torch.empty(n, dtype=torch.int32, device=dev)
+        hdr = torch.empty(n, dtype=torch.int32, device=dev)
+        ok, nbad = vc.verify_frames(d, off=torch.from_numpy(offs.view(np.int64)).to(dev),
+                                    length=torch.from_numpy(lens.view(np.int32)).to(dev), out_crc=crc, out_hdr=hdr,
+                                    len_hint=1200)
+        torch.cuda.synchronize()
+    finally:
+        vc.set_geometry()
+    assert int(nbad.item()) == 97
+    assert np.array_equal(ok.cpu().numpy(), want_ok)
+    crc2, hdr2 = _oracle.frames(base, offs, lens, header=True, nthreads=16)
+    assert np.array_equal(_u32(crc), crc2) and np.array_equal(_u32(hdr), hdr2)
+
+
 def _ragged_fast(seed, n, lo, hi):
     rng = np.random.default_rng(seed)
     lens = rng.integers(lo, hi + 1, n).astype(np.uint32)
