@@ -967,6 +967,10 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     const uint32_t nwp = ((gridDim.x - part + P - 1) / P) * kWavesPerBlock;  // waves of this partition
     uint32_t *head = p.heads + part * 16u;  // 64 B apart
     const uint32_t k0 = (blockIdx.x / P) * kWavesPerBlock + (threadIdx.x >> 6);
+    // (Dealing the first half or three quarters of every wave's items
+    // statically, as the uniform kernel does, lost on mixes: cfg5 -1.2% and
+    // -3.1%, class-2 mix -0.7% and -2%; uniform 16,400-B frames +1.3% and
+    // +0.7%; profiles/r04_ab_ragged_static_prefix.log.)
     uint32_t it = part + P * k0;
     if (it >= items) return;
     Item cur = ragged_item(ctab, it);
