@@ -748,6 +748,10 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
 //   class 1 (G=4,  256 B rounds): L in [1024, 8192)    buckets 8..36
 //   class 2 (G=8,  512 B rounds): L in [8192, 49152)   buckets 37..117
 //   class 3 (G=16, 1 KiB rounds): L in [49152, 65536]  buckets 118..134, longer 135
+// (Buckets of two rounds for classes 1 and 2, so that an item's frames lie
+// closer together in memory at the price of one idle round for some lanes,
+// measured neutral: cfg5 0 / -0.2%, class-2 mix +0.5%;
+// profiles/r04_ab_ragged_two_round_buckets.log.)
 constexpr int kBuckets = 136;
 __host__ __device__ inline int length_bucket(uint32_t L)
 {
