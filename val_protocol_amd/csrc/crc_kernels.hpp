@@ -975,7 +975,17 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     // statically, as the uniform kernel does, lost on mixes: cfg5 -1.2% and
     // -3.1%, class-2 mix -0.7% and -2%; uniform 16,400-B frames +1.3% and
     // +0.7%; profiles/r04_ab_ragged_static_prefix.log.)
-    uint32_t it = part + P * k0;
+    // Partition part's idx-th item. A one-bucket batch (uniform lengths without
+    // a length hint, identity order) deals its items to the partitions in runs
+    // of 4 consecutive items, so a partition's waves (one XCD) hash neighbouring
+    // frames: u16400 +2.8%, u600 +1.4% through this path. Mixes keep runs of 1:
+    // there runs of 4 measured -0.1 to -0.4% and runs of 16 -1.5 to -2.6%
+    // (profiles/r04_ab_ragged_item_runs.log).
+    const uint32_t lgch = ident ? 2u : 0u;
+    auto item_of = [&](uint32_t idx) {
+        return (((idx >> lgch) * P + part) << lgch) + (idx & ((1u << lgch) - 1u));
+    };
+    uint32_t it = item_of(k0);
     if (it >= items) return;
     Item cur = ragged_item(ctab, it);
     uint64_t f, off;
@@ -1001,7 +1011,7 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
         // -2.4%, 1,100-B frames -16%; with the unit loads -0.3 to -7%;
         // profiles/r04_ab_ragged_compile_time_lanes.log.)
         hash_frame<0, PF, PAY, false>(p, f, active, off, L, lane & (G - 1), sb, G, [] {}, [&] {
-            it_n = part + P * (__builtin_amdgcn_readfirstlane(k_n) + nwp);
+            it_n = item_of(__builtin_amdgcn_readfirstlane(k_n) + nwp);
             if (it_n < items) {
                 nx = ragged_item(ctab, it_n);
                 item_frame(p, nx, lane, f_n, active_n, off_n, L_n, ident);
