@@ -708,6 +708,9 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
     }
     uint32_t k = 0;
     if (P > 1u && ql == 0) k = atomicAdd(&p.qhead[part * 16u], 1u);
+    // (Runs of 4 or 16 consecutive groups per partition, as the ragged kernel
+    // deals one-bucket batches, measured neutral here: -0.4 to +0.4%;
+    // profiles/r04_ab_dyn_tail_runs.log.)
     uint64_t gb = P == 1u ? p.n : dyn + ((uint64_t)part + (uint64_t)P * __builtin_amdgcn_readfirstlane(k)) * kGroups;
     uint64_t fd = gb + (uint64_t)(ql / G), od = 0;
     uint32_t Ld = 0;
