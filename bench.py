@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--pay", action="store_true", help="with --verify: also emit payload states (RX file-CRC by-product)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
-    ap.add_argument("--host-inclusive", action="store_true", help="also time H2D+kernel+D2H (stderr)")
+    ap.add_argument("--no-host-inclusive", action="store_true",
+                    help="skip the host-inclusive block (H2D + kernel + D2H through val_crc32_frames_host)")
     ap.add_argument("--sort-frames", action="store_true", help="cfg5: order descriptors by length (diagnostic)")
     ap.add_argument("--no-cfg4-strong", action="store_true",
                     help="skip the cfg4 strong-scaling block (BASELINE configs[3]) timed after the headline")
@@ -211,15 +212,26 @@ def cpu_baseline(sample: np.ndarray, n: int, threads: int, stride: int = 0, flen
 
 def read_pmc_traffic(config: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    workload (profiles/pmc_<config>.json, produced by tools/pmc_traffic.py),
-    or None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    workload (profiles/pmc_<config>.json, tools/pmc_traffic.py) and where it
+    came from. PMC counters need their own rocprofv3 passes, so the number is
+    never measured by this run: `traffic_source` names the file, the tree and
+    box it was measured on, and whether the library this run loaded was built
+    from the same sources (val_protocol_amd/libval_crc_hip.so.srchash)."""
+    rel = os.path.join("profiles", f"pmc_{config}.json")
     try:
-        with open(p) as f:
+        with open(os.path.join(ROOT, rel)) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
     except Exception:
-        return None
+        return None, None
+    src = dict(d.get("source") or {})
+    try:
+        with open(os.path.join(ROOT, "val_protocol_amd", "libval_crc_hip.so.srchash")) as f:
+            mine = f.read().strip()
+    except OSError:
+        mine = None
+    src.update({"file": rel, "measured_in_this_run": False,
+                "same_library_sources": bool(mine) and src.get("lib_srchash") == mine})
+    return d.get("hbm_bytes_per_launch"), src
 
 
 def read_roof(torch, flat, stream):
@@ -247,6 +259,63 @@ def read_roof(torch, flat, stream):
         torch.cuda.synchronize()
         ms.append(a.elapsed_time(b))
     return nbytes / (float(np.median(ms)) * 1e-3) / 1e9
+
+
+def host_inclusive(vc, w, slice_bytes=1 << 30, reps=3):
+    """The path as VAL runs it: frames in host memory (the transport's byte
+    stream), CRCs back in host memory. A >= 1 GiB slice of this run's own
+    frames (CRC input) goes through the C-ABI host call
+    val_crc32_frames_host from pinned memory (val_gpu_host_alloc: DMA in
+    place) and from pageable memory (bounced through pinned buffers): H2D in
+    64 MiB chunks overlapped with the kernel, then one D2H of the results.
+    Best of `reps` timed calls after one warm call; outputs are checked
+    against the device-resident launch's CRCs of the same frames."""
+    import torch
+
+    n, desc = w["n"], w["desc"]
+    if desc:
+        offs = w["d_off"].cpu().numpy().astype(np.uint64)
+        lens = w["d_len"].cpu().numpy().astype(np.uint32)
+        ends = offs + lens.astype(np.uint64)
+        cum = np.cumsum(lens.astype(np.int64))
+        ns = int(min(n, np.searchsorted(cum, slice_bytes) + 1))
+        span = int(ends[:ns].max()) + 4
+        host = w["flat"][:span].cpu().numpy()
+        kw = dict(off=offs[:ns], length=lens[:ns])
+        crc_bytes = int(cum[ns - 1])
+    else:
+        flen = w["flen"]
+        ns = int(min(n, -(-slice_bytes // flen)))
+        host = w["buf"][:ns].cpu().numpy().reshape(-1)
+        kw = dict(stride=w["stride"], flen=flen, n=ns)
+        crc_bytes = ns * flen
+    want = w["crc"][:ns].cpu().numpy().view(np.uint32)
+    pinned = vc.PinnedBuffer(host.size)
+    pinned.array[:] = host
+    before = vc.cpu_batch_count()
+    out = {"slice_frames": ns, "slice_crc_input_bytes": crc_bytes, "slice_wire_bytes": int(host.size),
+           "chunk_bytes": 64 << 20, "unit": "GiB/s", "reps": reps,
+           "path": "val_crc32_frames_host: H2D (64 MiB chunks on a copy stream, overlapped with the kernel) + "
+                   "kernel + D2H of the CRCs; GiB/s of CRC input, best of reps"}
+    ok = True
+    for kind, arr in (("pinned", pinned.array), ("pageable", host)):
+        crc = vc.frames_host(arr, **kw)  # warm: bounce buffers, descriptors
+        ok = ok and bool(np.array_equal(crc, want))
+        best = float("inf")
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            vc.frames_host(arr, **kw)
+            best = min(best, time.perf_counter() - t0)
+        out[kind] = round(crc_bytes / best / GIB, 2)
+        out[f"{kind}_ms"] = round(best * 1e3, 3)
+    pinned.free()
+    torch.cuda.synchronize()
+    out["value"] = out["pinned"]
+    out["outputs_equal_device"] = ok
+    out["on_gpu"] = vc.cpu_batch_count() == before  # no call was routed to the CPU engine
+    print(f"[bench] host-inclusive: pinned {out['pinned']} GiB/s, pageable {out['pageable']} GiB/s "
+          f"({ns} frames, {crc_bytes / GIB:.2f} GiB)", file=sys.stderr)
+    return out
 
 
 def build_workload(torch, dev, config, rank, world, verify, vc):
@@ -513,16 +582,12 @@ def main():
     total_bytes = (w["job_bytes"] if strong else bytes_per_launch * world) * args.steps
     value = total_bytes / elapsed_max / GIB
     achieved_gbs = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
+    traffic, traffic_src = read_pmc_traffic(args.config + ("_verify" if args.verify else ""))
     roof = read_roof(torch, flat, stream) if rank == 0 else None
 
-    if args.host_inclusive and rank == 0 and not ragged:
-        host = buf.cpu().numpy().reshape(-1)
-        t1 = time.perf_counter()
-        for _ in range(2):
-            vc.frames_host(host, stride=stride, flen=flen, n=n)
-        hi = 2 * bytes_per_launch / (time.perf_counter() - t1) / GIB
-        print(f"[bench] host-inclusive (pageable H2D + kernel + D2H): {hi:.2f} GiB/s", file=sys.stderr)
+    host_incl = None
+    if rank == 0 and not args.no_host_inclusive and not args.verify and not args.sort_frames:
+        host_incl = host_inclusive(vc, w)
 
     windows = verify_windows(torch, vc, flat, dev, stream) if ragged and rank == 0 else None
 
@@ -626,6 +691,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": bytes_per_launch,
                 # same box, same buffer: plain read-only stream (bench/roof.hip); SURVEY 8(d)
@@ -637,6 +703,9 @@ def main():
                 "read_roof_frac_of_peak": round(roof / HBM_PEAK_GBS, 4) if roof else None,
             },
             "cpu_baseline": cpu,
+            # north_star: the path starts and ends in host memory; this is the rate
+            # with the H2D and D2H copies (never `value`)
+            "host_inclusive": host_incl,
             # per-GPU rates and the aggregate's denominator (BASELINE configs[3])
             "per_rank": per_rank,
             "aggregate_over_max_rank": aggregate(per_rank, total_bytes, elapsed_max),

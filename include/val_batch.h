@@ -1,0 +1,98 @@
+/*
+ * val_batch.h -- window batching of VAL's per-frame CRCs at the two hooks
+ * the reference already exposes, with no change to its sources.
+ *
+ * The reference hashes one frame per call and sends it at once: TX frames
+ * are built in the single send_buffer, CRC'd by val_internal_crc32 and
+ * handed to transport.send (src/val_core.c:718-866, called W times per
+ * window fill by src/val_sender.c:822-841); RX reads header, content and
+ * trailer with three transport.recv calls and CRCs the frame in recv_buffer
+ * (src/val_core.c:880-1073, called once per frame by the data loop of
+ * src/val_receiver.c:801-1047). val_batch_attach() wraps a session's
+ * val_config_t before val_session_create so that
+ *
+ *   TX: the CRC provider (val_config_t.crc32_provider, include/
+ *       val_protocol.h:264-266) returns a placeholder for frames built in
+ *       send_buffer, and the wrapped transport.send stages each frame in a
+ *       window buffer instead of sending it. A window is flushed before the
+ *       session next reads (the sender waits for ACKs after every window
+ *       fill), when a control frame is sent, on transport.flush, or when the
+ *       window buffer is full: the trailers of all staged frames come from
+ *       ONE val_crc32_frames_host call, are written little-endian, and the
+ *       frames go to the application's transport in order. The wire is the
+ *       reference's, byte for byte; only the time of sending moves to the
+ *       end of the window fill.
+ *   RX: the wrapped transport.recv reads ahead: the frame the session asked
+ *       for plus every further frame the transport already holds (polled
+ *       with a zero timeout), up to the window limits, and computes their
+ *       CRCs with ONE val_crc32_frames_host call. It hands bytes to the
+ *       session exactly as asked; when a frame's header and content were
+ *       delivered to recv_buffer in place and its trailer after them, the
+ *       provider call that follows (src/val_core.c:964) is answered with
+ *       that frame's batch CRC. Every other provider call (resume windows,
+ *       frames split across read-aheads) is computed directly.
+ *
+ * The application keeps its own transport and provider semantics: the
+ * wrapped hooks call the ones in the config at attach time (a NULL provider
+ * means this library's val_gpu_crc32_provider). Batches below the host-batch
+ * crossover run on the CPU engine (val_gpu_host_batch_min_bytes), larger
+ * ones on the GPU; VAL_GPU_HOST_BATCH_MIN_BYTES=0 sends every window to the
+ * GPU.
+ */
+#ifndef VAL_BATCH_H
+#define VAL_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "val_errors.h"
+#include "val_protocol.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    uint32_t max_frames;  /* frames per batch, TX and RX (0 = 65,535) */
+    size_t max_bytes;     /* wire bytes per batch (0 = 16 MiB; at least one MTU) */
+    int tx;               /* 1: defer TX trailers to window batches */
+    int rx;               /* 1: read ahead and hash RX frames in batches */
+    int coalesce_send;    /* 1: one transport.send per flushed window (0: one per frame, as the reference) */
+} val_batch_opts_t;
+
+typedef struct {
+    uint64_t tx_frames;          /* frames passed to the application's transport.send */
+    uint64_t tx_batched_frames;  /* of those, trailers computed in a window batch */
+    uint64_t tx_batches;         /* window batches (one frames_host call each) */
+    uint64_t tx_max_batch;       /* most frames in one TX batch */
+    uint64_t rx_frames;          /* complete frames read ahead */
+    uint64_t rx_batches;         /* RX batches (one frames_host call each) */
+    uint64_t rx_max_batch;       /* most frames in one RX batch */
+    uint64_t rx_batched_answers; /* provider calls answered from an RX batch */
+    uint64_t direct_answers;     /* provider calls computed directly (resume windows, split frames) */
+    int32_t status;              /* first transport or batch failure (VAL_OK if none) */
+} val_batch_stats_t;
+
+typedef struct val_batch val_batch_t;
+
+/* Wrap cfg->transport and cfg->crc32_provider (cfg->buffers.send_buffer,
+ * recv_buffer and packet_size must be set). opts may be NULL (defaults: TX
+ * and RX batching on). cfg must outlive the session; call
+ * val_batch_detach after val_session_destroy. Up to 256 attached configs
+ * per process. */
+val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out);
+/* Send the staged TX window now (the wrapped hooks do this themselves). */
+val_status_t val_batch_flush(val_batch_t *b);
+void val_batch_get_stats(const val_batch_t *b, val_batch_stats_t *out);
+/* Flush, restore cfg's hooks and free the batcher. */
+void val_batch_detach(val_batch_t *b);
+/* The provider val_batch_attach installs (crc32_func_t): a placeholder for a
+ * frame in an attached send_buffer, the batch CRC of a frame delivered in
+ * place to an attached recv_buffer, else val_gpu_crc32_provider semantics. */
+uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VAL_BATCH_H */

@@ -186,8 +186,15 @@ uint64_t val_gpu_host_batch_min_bytes(void);
 uint64_t val_gpu_cpu_batch_count(void);
 /* Threads the CPU engine uses for one such batch: the calling thread plus
  * threads - 1 helpers over byte-balanced frame ranges, at most one thread
- * per 4 MiB of CRC input (default 1). */
+ * per 4 MiB of CRC input (default 1), never more than the process's CPU
+ * budget (its affinity set capped by the cgroup CPU quota). */
 void val_gpu_set_host_cpu_threads(uint32_t threads);
+/* The *_host_multi calls decide CPU or GPU once for the whole batch: below
+ * val_gpu_host_batch_min_bytes() * T / N bytes of CRC input, with N the
+ * distinct devices the shards land on and T the CPU engine's threads, the
+ * CPU engine answers it. Returns that threshold for
+ * `devices` devices. */
+uint64_t val_gpu_host_multi_min_bytes(int devices);
 
 /* Host-memory form of val_crc32_verify_frames_ex_dev (pay: n entries, nullable). */
 val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,

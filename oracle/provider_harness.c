@@ -36,11 +36,20 @@
  *   provider_harness none sessions
  *       writes tests/golden/session_vectors.json (see mode_sessions): windowed
  *       and resumed reference sessions, every frame logged.
- *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu>
+ *   provider_harness <libval_crc_hip.so|none> loopback <bytes> <mtu> [window]
  *       full val_send_files / val_receive_files transfer over an in-memory
  *       duplex pipe (the reference test strategy), provider on
  *       both sessions ("none" = reference built-in CRC). Prints a digest of
- *       every frame put on the wire so runs can be compared bit for bit.
+ *       every frame put on the wire so runs can be compared bit for bit, and
+ *       how many logged trailers equal the reference's own val_crc32.
+ *   provider_harness <libval_crc_hip.so> loopback-batched <bytes> <mtu> <window>
+ *       the same transfer with the product's window batcher attached to both
+ *       configs (include/val_batch.h: TX trailers from one frames_host call
+ *       per window fill, RX frames read ahead and checked from one call).
+ *   provider_harness <libval_crc_hip.so> sessions | sessions-batched
+ *       the five recorded sessions of `none sessions` (windowed, resumed)
+ *       re-run with the product's provider installed, plain or batched;
+ *       same output format plus the product-side counters.
  * Output: one JSON object per line.
  */
 #define _GNU_SOURCE
@@ -77,6 +86,8 @@ static void delay(uint32_t ms)
     struct timespec ts = {ms / 1000u, (long)(ms % 1000u) * 1000000L};
     nanosleep(&ts, NULL);
 }
+
+static uint32_t le32(const uint8_t *p);
 
 /* ---- in-memory byte pipe ------------------------------------------------ */
 typedef struct {
@@ -306,6 +317,63 @@ typedef int (*fn_scan_t)(const uint8_t *, size_t, size_t, uint32_t, uint64_t *, 
 typedef int (*fn_verify_t)(const uint8_t *, uint64_t, const uint64_t *, const uint32_t *, uint64_t, uint32_t, uint32_t,
                            uint8_t *, uint32_t *);
 static void *g_lib;
+
+/* The product's window batcher (include/val_batch.h), reached through dlsym;
+ * its two structs restated here because this file compiles against the
+ * reference's headers. */
+typedef struct {
+    uint32_t max_frames;
+    size_t max_bytes;
+    int tx, rx, coalesce_send;
+} hb_opts_t;
+typedef struct {
+    uint64_t tx_frames, tx_batched_frames, tx_batches, tx_max_batch, rx_frames, rx_batches, rx_max_batch,
+        rx_batched_answers, direct_answers;
+    int32_t status;
+} hb_stats_t;
+typedef int (*fn_battach_t)(val_config_t *, const hb_opts_t *, void **);
+typedef void (*fn_bdetach_t)(void *);
+typedef void (*fn_bstats_t)(const void *, hb_stats_t *);
+typedef uint64_t (*fn_count_t)(void);
+
+static uint64_t lib_count(const char *name)
+{
+    fn_count_t f = g_lib ? (fn_count_t)dlsym(g_lib, name) : NULL;
+    return f ? f() : 0;
+}
+
+/* Attach the batcher to both ends' configs (before val_session_create). */
+static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
+{
+    fn_battach_t at = (fn_battach_t)dlsym(g_lib, "val_batch_attach");
+    if (!at) return -1;
+    hb_opts_t o = {0, 0, 1, 1, 0};
+    if (at(a, &o, ba) != 0 || at(b, &o, bb) != 0) return -1;
+    return 0;
+}
+
+static void batch_report(void *ba, void *bb)
+{
+    fn_bstats_t gs = (fn_bstats_t)dlsym(g_lib, "val_batch_get_stats");
+    fn_bdetach_t dt = (fn_bdetach_t)dlsym(g_lib, "val_batch_detach");
+    hb_stats_t st[2];
+    memset(st, 0, sizeof st);
+    gs(ba, &st[0]);
+    gs(bb, &st[1]);
+    printf(",\"batch\":[");
+    for (int k = 0; k < 2; k++)
+        printf("%s{\"end\":\"%s\",\"tx_frames\":%llu,\"tx_batched_frames\":%llu,\"tx_batches\":%llu,\"tx_max_batch\":%llu,"
+               "\"rx_frames\":%llu,\"rx_batches\":%llu,\"rx_max_batch\":%llu,\"rx_batched_answers\":%llu,"
+               "\"direct_answers\":%llu,\"status\":%d}",
+               k ? "," : "", k ? "receiver" : "sender", (unsigned long long)st[k].tx_frames,
+               (unsigned long long)st[k].tx_batched_frames, (unsigned long long)st[k].tx_batches,
+               (unsigned long long)st[k].tx_max_batch, (unsigned long long)st[k].rx_frames,
+               (unsigned long long)st[k].rx_batches, (unsigned long long)st[k].rx_max_batch,
+               (unsigned long long)st[k].rx_batched_answers, (unsigned long long)st[k].direct_answers, st[k].status);
+    printf("]");
+    dt(ba);
+    dt(bb);
+}
 
 static int mode_window(uint32_t W, size_t mtu)
 {
@@ -568,7 +636,20 @@ static void *rx_main(void *arg)
     return NULL;
 }
 
-static int mode_loopback(size_t bytes, size_t mtu, int use_gpu)
+/* Every frame an end put on the wire carries the reference's own CRC
+ * (val_crc32 of this binary) as its trailer: counted over the frame log. */
+static unsigned long trailers_ok(const end_t *e)
+{
+    unsigned long n = 0;
+    for (size_t i = 0; i < e->nlog; i++) {
+        const uint8_t *f = e->log[i].bytes;
+        const size_t wl = e->log[i].len;
+        n += wl >= 12 && val_crc32(f, wl - 4) == le32(f + wl - 4);
+    }
+    return n;
+}
+
+static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window, int batched)
 {
     char tmpl[] = "/tmp/valgpuXXXXXX";
     char *dir = mkdtemp(tmpl);
@@ -587,11 +668,22 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu)
     pipe_t a2b, b2a;
     pipe_init(&a2b, 64u << 20);
     pipe_init(&b2a, 64u << 20);
-    end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0};
+    end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0, NULL, 0, 0, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0, NULL, 0, 0, 0};
+    etx.caplog = erx.caplog = 4096;
+    etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
+    erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
     crc32_func_t prov = use_gpu ? counting_provider : NULL;
     val_config_t ctx_, crx;
     make_cfg(&ctx_, &etx, mtu, prov);
     make_cfg(&crx, &erx, mtu, prov);
+    if (window) {
+        ctx_.tx_flow.window_cap_packets = crx.tx_flow.window_cap_packets = window;
+        ctx_.tx_flow.initial_cwnd_packets = crx.tx_flow.initial_cwnd_packets = window;
+    }
+    void *ba = NULL, *bb = NULL;
+    const uint64_t cpu_b0 = lib_count("val_gpu_cpu_batch_count"), cpu_s0 = lib_count("val_gpu_cpu_small_count"),
+                   cpu_f0 = lib_count("val_gpu_cpu_fallback_count");
+    if (batched && batch_attach(&ctx_, &crx, &ba, &bb) != 0) return 4;
     val_session_t *tx = NULL, *rx = NULL;
     if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
     rx_job_t job = {rx, outdir, VAL_OK};
@@ -616,13 +708,25 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu)
         equal = (r == bytes) && memcmp(back, data, bytes) == 0;
         free(back);
     }
-    printf("{\"mode\":\"loopback\",\"gpu\":%d,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,\"rx_status\":%d,\"equal\":%d,"
+    printf("{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
+           "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
-           "\"tx_digest\":%u,\"rx_digest\":%u,\"provider_calls\":%lu,\"wall_ms\":%u}\n",
-           use_gpu, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
-           mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu, g_calls, t1 - t0);
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
+           "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
+           use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
+           mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
+           trailers_ok(&etx) + trailers_ok(&erx), g_calls, t1 - t0,
+           (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
+           (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
+           (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
     val_session_destroy(tx);
     val_session_destroy(rx);
+    if (batched) batch_report(ba, bb);
+    printf("}\n");
+    for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
+    for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
+    free(etx.log);
+    free(erx.log);
     remove(out);
     remove(in);
     rmdir(outdir);
@@ -990,7 +1094,7 @@ static void fx_log_epochs(const end_t *e, const uint8_t *file, size_t bytes)
  * the receiver's output file starts as the input's first `existing` bytes
  * (byte `flip` XOR 0x5A when flip >= 0). */
 static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t window, uint32_t tail_cap, size_t existing,
-                      long long flip, uint64_t seed, int last)
+                      long long flip, uint64_t seed, int last, crc32_func_t prov, int batched)
 {
     char tmpl[] = "/tmp/valssXXXXXX";
     char *dir = mkdtemp(tmpl);
@@ -1021,11 +1125,15 @@ static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t windo
     etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
     erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
     val_config_t ctx_, crx;
-    make_cfg(&ctx_, &etx, mtu, NULL);
-    make_cfg(&crx, &erx, mtu, NULL);
+    make_cfg(&ctx_, &etx, mtu, prov);
+    make_cfg(&crx, &erx, mtu, prov);
     ctx_.tx_flow.window_cap_packets = crx.tx_flow.window_cap_packets = window;
     ctx_.tx_flow.initial_cwnd_packets = crx.tx_flow.initial_cwnd_packets = window;
     ctx_.resume.tail_cap_bytes = crx.resume.tail_cap_bytes = tail_cap;
+    void *ba = NULL, *bb = NULL;
+    const uint64_t cpu_b0 = lib_count("val_gpu_cpu_batch_count"), cpu_s0 = lib_count("val_gpu_cpu_small_count"),
+                   cpu_f0 = lib_count("val_gpu_cpu_fallback_count");
+    if (batched && batch_attach(&ctx_, &crx, &ba, &bb) != 0) return 4;
     val_session_t *tx = NULL, *rx = NULL;
     if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
     rx_job_t job = {rx, outdir, VAL_OK};
@@ -1056,9 +1164,19 @@ static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t windo
     fx_log_epochs(&etx, data, bytes);
     printf("],\"rx_frames\":[");
     fx_log_epochs(&erx, data, bytes);
-    printf("]}%s\n", last ? "" : ",");
+    printf("]");
+    if (prov) {  /* the product installed: every logged trailer against the reference's own val_crc32 */
+        printf(",\"provider\":\"%s\",\"trailers_ok\":%lu,\"frames_logged\":%zu,\"lib_cpu_batches\":%llu,"
+               "\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
+               batched ? "batched" : "product", trailers_ok(&etx) + trailers_ok(&erx), etx.nlog + erx.nlog,
+               (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
+               (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
+               (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
+    }
     val_session_destroy(tx);
     val_session_destroy(rx);
+    if (batched) batch_report(ba, bb);
+    printf("}%s\n", last ? "" : ",");
     for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
     for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
     free(etx.log);
@@ -1072,16 +1190,20 @@ static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t windo
     return 0;
 }
 
-static int mode_sessions(void)
+/* prov NULL: the reference's built-in CRC (the recorded fixtures); else the
+ * product's provider installed on both ends, optionally with the batcher. */
+static int mode_sessions(crc32_func_t prov, int batched)
 {
     int rc = 0;
-    printf("{\"generator\":\"oracle/provider_harness none sessions (reference src/ built by oracle/Makefile, built-in CRC)\",\n"
-           "\"sessions\":[\n");
-    rc |= fx_session("window64_mtu1024", 600000, 1024, 64, 1024, 0, -1, 0x5E55101, 0);
-    rc |= fx_session("window64_mtu16404", 3u << 20, 16404, 64, 1024, 0, -1, 0x5E55102, 0);
-    rc |= fx_session("resume_tail_cap8m", (12u << 20) + 777u, 4096, 16, 0, (10u << 20) + 12345u, -1, 0x5E55103, 0);
-    rc |= fx_session("resume_tail_cap1k", 400000, 1024, 8, 1024, 300005, -1, 0x5E55104, 0);
-    rc |= fx_session("resume_tail_mismatch", 400000, 1024, 8, 8192, 300005, 300005 - 100, 0x5E55105, 1);
+    printf("{\"generator\":\"oracle/provider_harness %s sessions (reference src/ built by oracle/Makefile, %s)\",\n"
+           "\"sessions\":[\n", prov ? "<lib>" : "none",
+           prov ? (batched ? "product provider + val_batch window batching" : "product provider") : "built-in CRC");
+    rc |= fx_session("window64_mtu1024", 600000, 1024, 64, 1024, 0, -1, 0x5E55101, 0, prov, batched);
+    rc |= fx_session("window64_mtu16404", 3u << 20, 16404, 64, 1024, 0, -1, 0x5E55102, 0, prov, batched);
+    rc |= fx_session("resume_tail_cap8m", (12u << 20) + 777u, 4096, 16, 0, (10u << 20) + 12345u, -1, 0x5E55103, 0, prov,
+                     batched);
+    rc |= fx_session("resume_tail_cap1k", 400000, 1024, 8, 1024, 300005, -1, 0x5E55104, 0, prov, batched);
+    rc |= fx_session("resume_tail_mismatch", 400000, 1024, 8, 8192, 300005, 300005 - 100, 0x5E55105, 1, prov, batched);
     printf("]}\n");
     return rc;
 }
@@ -1089,7 +1211,7 @@ static int mode_sessions(void)
 int main(int argc, char **argv)
 {
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
-    if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions();
+    if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions(NULL, 0);
     if (argc < 3) {
         fprintf(stderr, "usage: %s <libval_crc_hip.so|none> tx|rx|loopback [bytes mtu]\n", argv[0]);
         return 1;
@@ -1104,8 +1226,15 @@ int main(int argc, char **argv)
         }
         g_gpu = (crc32_func_t)dlsym(h, "val_gpu_crc32_provider");
         int (*init)(int) = (int (*)(int))dlsym(h, "val_gpu_init");
-        if (!g_gpu || !init || init(0) != 0) {
+        if (!g_gpu || !init) {
             fprintf(stderr, "GPU provider unavailable\n");
+            return 1;
+        }
+        /* Without a device the product still answers below its thresholds
+           (its CPU engine); the tx/rx/window modes need the GPU. */
+        const int have_gpu = init(0) == 0;
+        if (!have_gpu && (!strcmp(argv[2], "tx") || !strcmp(argv[2], "rx") || !strncmp(argv[2], "window", 6))) {
+            fprintf(stderr, "no HIP device\n");
             return 1;
         }
         (void)g_gpu(0xFFFFFFFFu, "warm", 4); /* first call pays HIP init, not the protocol */
@@ -1120,7 +1249,14 @@ int main(int argc, char **argv)
                                           atoi(argv[5]))
                        : 1;
     if (!strcmp(argv[2], "loopback") && argc >= 5)
-        return mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu);
+        return mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu,
+                             argc >= 6 ? (uint16_t)strtoul(argv[5], NULL, 0) : 0, 0);
+    if (!strcmp(argv[2], "loopback-batched") && argc >= 6)
+        return use_gpu ? mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), 1,
+                                       (uint16_t)strtoul(argv[5], NULL, 0), 1)
+                       : 1;
+    if (!strcmp(argv[2], "sessions")) return use_gpu ? mode_sessions(counting_provider, 0) : 1;
+    if (!strcmp(argv[2], "sessions-batched")) return use_gpu ? mode_sessions(counting_provider, 1) : 1;
     fprintf(stderr, "bad mode\n");
     return 1;
 }

@@ -17,7 +17,7 @@ INC = os.path.join(ROOT, "include")
 
 def _declared_functions():
     names = set()
-    for h in ("val_crc32_gpu.h", "val_protocol.h", "val_wire.h"):
+    for h in ("val_crc32_gpu.h", "val_protocol.h", "val_wire.h", "val_batch.h"):
         txt = open(os.path.join(INC, h)).read()
         # the session API is the reference's control plane, declared for its sources, not exported here
         txt = re.sub(r"/\* control-plane API begin \*/.*?/\* control-plane API end \*/", "", txt, flags=re.S)

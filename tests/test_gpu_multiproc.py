@@ -31,12 +31,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _bench_two_ranks(config: str, *extra: str) -> dict:
+def _bench_two_ranks(config: str, *extra: str, ranks: int = 2, timeout: int = 240) -> dict:
     env = dict(os.environ, VAL_BENCH_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline", *extra]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+           "--gpus", str(ranks), "--config", config, "--steps", "2", "--warmup", "1", "--no-cpu-baseline", *extra]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints exactly one line
@@ -70,6 +70,32 @@ def test_bench_two_ranks_weak_cfg2():
     assert st["value"] > 0
 
 
+def test_bench_eight_ranks_rehearsal():
+    """The driver's 8-GPU invocation rehearsed on one GPU: 8 ranks under
+    torch.distributed.run (gloo for the host-side collectives, all on
+    cuda:0), cfg2 weak plus the cfg4 strong block: the 8 GiB file's 131,113
+    frames split byte-balanced (~16,389 per rank, no collective on the data),
+    the 816-B last frame on rank 7, the aggregate over the slowest rank, and
+    every rank's parity sample against the oracle."""
+    line = _bench_two_ranks("cfg2", "--with-cfg4-strong", "--no-host-inclusive", ranks=8, timeout=170)
+    assert line["n_gpus"] == 8 and line["scaling"] == "weak" and line["config"]["parity_sample_ok"] is True
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8)) and all(r["parity_sample_ok"] for r in pr)
+    assert line["aggregate_over_max_rank"]["total_bytes"] == 8 * 2 * 65536 * (8 + 8 + 1024)
+    st = line["cfg4_strong"]
+    spr = st["per_rank"]
+    assert st["parity_sample_ok"] is True and [r["rank"] for r in spr] == list(range(8))
+    assert sum(r["frames"] for r in spr) == 131113
+    assert all(16387 <= r["frames"] <= 16391 for r in spr), [r["frames"] for r in spr]
+    assert spr[7]["last_frame_crc_input"] == 8 + 8 + 800
+    assert all(r["last_frame_crc_input"] == 8 + 8 + 65516 for r in spr[:7])
+    file_crc_input = 131112 * (8 + 8 + 65516) + 8 + 8 + 800
+    agg = st["aggregate_over_max_rank"]
+    assert agg["total_bytes"] == 2 * file_crc_input
+    assert agg["max_elapsed_s"] == max(r["elapsed_s"] for r in spr)
+    assert abs(st["value"] - agg["total_bytes"] / agg["max_elapsed_s"] / 2**30) / st["value"] < 0.01
+
+
 def test_bench_rccl_process_group_one_rank():
     """The RCCL (nccl backend) code path of bench.py on real hardware: one rank
     under torch.distributed.run with a process group forced on, so the nccl
@@ -87,6 +113,10 @@ def test_bench_rccl_process_group_one_rank():
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["config"]["parity_sample_ok"] is True and line["value"] > 0
+    # the host-inclusive block (north_star: H2D + kernel + D2H through the C ABI)
+    hi = line["host_inclusive"]
+    assert hi["outputs_equal_device"] is True and hi["on_gpu"] is True, hi
+    assert hi["pinned"] > 0 and hi["pageable"] > 0 and hi["slice_frames"] == 65536
     assert [x["rank"] for x in line["per_rank"]] == [0]
     st = line["cfg4_strong"]
     assert st["parity_sample_ok"] is True and st["per_rank"][0]["frames"] == 131113

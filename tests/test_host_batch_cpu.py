@@ -124,6 +124,72 @@ def test_strided_and_payload_states(cpu_routed):
         assert int(pay[i]) == exp, i
 
 
+def test_helper_threads_large_batches(cpu_routed):
+    """Batches of >= 16 MiB of CRC input, where the 4-thread parametrization
+    really starts helper threads (one per 4 MiB): strided, descriptor (mixed
+    lengths, so the byte-balanced cuts differ from count cuts) and verify with
+    corruption on both sides of a cut, against the oracle."""
+    n, flen, stride = 16400, 1040, 1044  # 17.1 MB of CRC input
+    sb = _prng.prng_bytes(94, n * stride)
+    want = _oracle.frames_strided(sb, stride, flen, n)
+    assert np.array_equal(vc.frames_host(sb, stride=stride, flen=flen, n=n), want)
+    rng = np.random.default_rng(95)
+    lens = rng.integers(1, 9000, 4000).astype(np.uint32)  # ~18 MB
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + 4)[:-1]]).astype(np.uint64)
+    base = _prng.prng_bytes(96, int(offs[-1]) + int(lens[-1]) + 4)
+    want = _oracle.frames(base, offs, lens)
+    assert np.array_equal(vc.frames_host(base, off=offs, length=lens), want)
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        base[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(int(want[i]).to_bytes(4, "little"), np.uint8)
+    bad = [3, 1999, 2000, 3999]
+    for i in bad:
+        base[int(offs[i])] ^= 0x40
+    st, ok, nbad = vc.verify_frames_host(base, off=offs, length=lens)
+    assert st == VAL_ERR_CRC and nbad == len(bad)
+    assert np.nonzero(ok == 0)[0].tolist() == bad
+    assert vc.cpu_batch_count() - cpu_routed == 3
+
+
+def _cpu_budget() -> int:
+    """The library's CPU budget: the affinity set capped by the cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except OSError:
+        pass
+    return n
+
+
+def test_multi_decides_once_for_the_whole_batch():
+    """val_crc32_*_host_multi choose CPU or GPU once per batch against a
+    crossover that scales with the distinct devices and the CPU threads
+    (C1 * T / N), never per shard; below it the batch needs no device (this
+    container has none) and the helper threads stay within the CPU budget."""
+    vc.set_host_batch_min_bytes(64 << 20)  # the built-in single-GPU crossover (conftest exports 0)
+    try:
+        assert vc.host_multi_min_bytes(1) == 64 << 20
+        assert vc.host_multi_min_bytes(8) == 8 << 20
+        vc.set_host_cpu_threads(4)
+        assert vc.host_multi_min_bytes(8) == min(4, _cpu_budget()) * (8 << 20)
+        vc.set_host_cpu_threads(1)
+        n, flen, stride = 2000, 1040, 1044
+        sb = _prng.prng_bytes(97, n * stride)
+        before = vc.cpu_batch_count()
+        for ndev in (0, 1, 3, 8):
+            got = vc.frames_host_multi(sb, stride=stride, flen=flen, n=n, ndev=ndev)
+            assert np.array_equal(got, _oracle.frames_strided(sb, stride, flen, n)), ndev
+        data = _prng.prng_bytes(98, (9 << 20) + 77)
+        vc.set_host_cpu_threads(4)  # 9 MiB: two ranges at most (one per 4 MiB)
+        for ndev in (1, 8):
+            assert vc.region_host_multi(data, ndev=ndev) == _oracle.update_state(0xFFFFFFFF, data)
+        assert vc.cpu_batch_count() - before == 6
+    finally:
+        vc.set_host_batch_min_bytes(-1)
+        vc.set_host_cpu_threads(1)
+
+
 def test_threshold_knob():
     vc.set_host_batch_min_bytes(12345)
     assert vc.host_batch_min_bytes() == 12345

@@ -6,7 +6,10 @@ hbm_read_bytes = FETCH_SIZE * 1024 * 2 (WRITE_SIZE taken as-is).
 Usage: pmc_traffic.py <fetch_csv> <write_csv|-> <cfg> <algorithmic_bytes_per_launch> [out.json]"""
 import csv
 import json
+import os
+import socket
 import sys
+import time
 from collections import defaultdict
 
 
@@ -16,6 +19,15 @@ def per_launch(path, counter):
         if "k_frames" in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return sum(vals.values()) / len(vals) if vals else None, len(vals)
+
+
+def _srchash():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        with open(os.path.join(root, "val_protocol_amd", "libval_crc_hip.so.srchash")) as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def main():
@@ -36,6 +48,15 @@ def main():
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": ((rd + wr) / alg) if rd is not None else None,
         "correction": "gfx950: FETCH_SIZE x1024 x2 (half-count of 16 B/lane streaming reads), WRITE_SIZE x1024",
+        # provenance: bench.py reports it beside the traffic and checks the
+        # library it loads was built from the same kernel sources
+        "source": {
+            "tree": os.environ.get("VAL_TREE", "unknown"),
+            "lib_srchash": _srchash(),
+            "box": socket.gethostname(),
+            "date": time.strftime("%Y-%m-%d %H:%M:%S"),
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes over tools/prof_target.py",
+        },
     }
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d))

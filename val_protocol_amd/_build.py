@@ -56,7 +56,7 @@ def is_current(out: str = OUT) -> bool:
 
 
 def build(verbose: bool = True, out: str = OUT, build_dir: str = BUILD) -> str:
-    """Compile val_wire.c and cpu_crc32.c (gcc) and val_crc32_hip.hip (hipcc, gfx950) and link
+    """Compile val_wire.c, val_batch.c and cpu_crc32.c (gcc) and val_crc32_hip.hip (hipcc, gfx950) and link
     ``out``. The library is linked to a temporary name and renamed, so a
     process that loads ``out`` meanwhile never sees a half-written file."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -65,16 +65,19 @@ def build(verbose: bool = True, out: str = OUT, build_dir: str = BUILD) -> str:
     wire_o = os.path.join(build_dir, "val_wire.o")
     hip_o = os.path.join(build_dir, "val_crc32_hip.o")
     cpu_o = os.path.join(build_dir, "cpu_crc32.o")
+    batch_o = os.path.join(build_dir, "val_batch.o")
     _run(["gcc", "-O2", "-fPIC", "-std=c99", "-Wall", "-Wextra", "-Werror", f"-I{INC}", "-c",
           os.path.join(CSRC, "val_wire.c"), "-o", wire_o], verbose)
     _run(["gcc", "-O3", "-fPIC", "-std=gnu99", "-Wall", "-Wextra", "-Werror", f"-I{CSRC}", "-c",
           os.path.join(CSRC, "cpu_crc32.c"), "-o", cpu_o], verbose)
+    _run(["gcc", "-O2", "-fPIC", "-std=c99", "-Wall", "-Wextra", "-Werror", f"-I{INC}", "-c",
+          os.path.join(CSRC, "val_batch.c"), "-o", batch_o], verbose)
     _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror", f"-I{INC}", f"-I{CSRC}",
           "-c", os.path.join(CSRC, "val_crc32_hip.hip"), "-o", hip_o], verbose)
     fd, tmp = tempfile.mkstemp(prefix=".libval_crc_hip.", suffix=".so", dir=os.path.dirname(out))
     os.close(fd)
     try:
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", tmp, hip_o, wire_o, cpu_o,
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", tmp, hip_o, wire_o, cpu_o, batch_o,
               "-lpthread"], verbose)
         os.chmod(tmp, 0o755)
         os.replace(tmp, out)

@@ -56,7 +56,8 @@ EXPORTS = (
     "val_crc32_fold_payload_states_at", "val_frame_data_offsets", "val_gpu_build_flags",
     "val_gpu_host_copy_threads", "val_gpu_set_ragged_min_frames", "val_gpu_ragged_min_frames",
     "val_gpu_scratch_entries", "val_gpu_set_host_batch_min_bytes", "val_gpu_host_batch_min_bytes",
-    "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads",
+    "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads", "val_gpu_host_multi_min_bytes",
+    "val_batch_attach", "val_batch_flush", "val_batch_get_stats", "val_batch_detach", "val_batch_crc32_provider",
     "val_serialize_handshake", "val_deserialize_handshake", "val_serialize_meta", "val_deserialize_meta",
     "val_serialize_resume_resp", "val_deserialize_resume_resp", "val_serialize_verify_request",
     "val_deserialize_verify_request", "val_serialize_verify_response", "val_deserialize_verify_response",
@@ -153,6 +154,7 @@ def _declare(lib: ctypes.CDLL, strict: bool = True) -> None:
     fn("val_gpu_host_batch_min_bytes", u64)
     fn("val_gpu_cpu_batch_count", u64)
     fn("val_gpu_set_host_cpu_threads", None, u32)
+    fn("val_gpu_host_multi_min_bytes", u64, ctypes.c_int)
 
 
 def lib() -> ctypes.CDLL:
@@ -264,6 +266,12 @@ def cpu_batch_count() -> int:
 def set_host_cpu_threads(threads: int) -> None:
     """Threads the CPU engine uses for one host batch below the threshold (default 1)."""
     lib().val_gpu_set_host_cpu_threads(int(threads))
+
+
+def host_multi_min_bytes(devices: int) -> int:
+    """CRC-input bytes below which a *_host_multi batch over `devices`
+    distinct GPUs is answered by the CPU engine (decided once per batch)."""
+    return int(lib().val_gpu_host_multi_min_bytes(int(devices)))
 
 
 def set_ragged_min_frames(frames: int) -> None:

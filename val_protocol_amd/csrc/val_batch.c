@@ -1,0 +1,495 @@
+/*
+ * val_batch.c -- window batching of VAL's per-frame CRCs through the
+ * reference's own hooks (include/val_batch.h). TX: placeholder trailers from
+ * the provider, frames staged by the wrapped transport.send and hashed in
+ * one val_crc32_frames_host call per window (reference src/val_core.c:
+ * 828-835, src/val_sender.c:822-841). RX: the wrapped transport.recv reads
+ * ahead whole frames, hashes them in one call, and the provider answers the
+ * session's per-frame check (src/val_core.c:963-974) from that batch.
+ */
+#include "val_batch.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "val_crc32_gpu.h"
+#include "val_wire.h"
+
+#define VB_MAX_ATTACHED 256
+#define VB_DEFAULT_BYTES ((size_t)16u << 20)
+#define VB_DEFAULT_FRAMES 65535u
+
+typedef struct {
+    uint64_t off;  /* in the window / ring buffer */
+    uint32_t len;  /* CRC input = wire - 4 */
+    uint32_t crc;  /* batch CRC (RX), or the trailer to write (TX) */
+    uint8_t need;  /* TX: trailer comes from the batch */
+} vb_frame_t;
+
+struct val_batch {
+    val_config_t *cfg;
+    /* the application's hooks, called by the wrappers */
+    int (*u_send)(void *, const void *, size_t);
+    int (*u_recv)(void *, void *, size_t, size_t *, uint32_t);
+    int (*u_is_connected)(void *);
+    void (*u_flush)(void *);
+    void *u_io;
+    crc32_func_t u_provider;
+    val_batch_opts_t opt;
+    const uint8_t *send_buffer, *recv_buffer;
+    size_t mtu;
+    int pinned;
+    /* TX window */
+    uint8_t *tx;
+    size_t tx_used;
+    vb_frame_t *txf;
+    uint32_t tx_n;
+    size_t tx_pending;  /* CRC input of the frame whose placeholder was just returned (0: none) */
+    /* RX ring: bytes [r_head, r_len) not yet handed to the session */
+    uint8_t *rx;
+    size_t r_head, r_len;
+    vb_frame_t *rxf;
+    uint32_t rx_n, rx_cur;  /* complete frames in the ring; the one being delivered */
+    uint64_t r_base;        /* stream position of rx[0] */
+    /* stream parse state: bytes still owed by the transport for the frame in
+       progress (0 = at a frame boundary), and whether a header is partial */
+    size_t owe;
+    uint8_t hdr_part[8];
+    size_t hdr_have;
+    int raw;  /* a header announced content beyond the MTU: no more read-ahead */
+    /* delivery of frame rx_cur into recv_buffer in place */
+    size_t cur_matched;
+    int armed;
+    uint32_t armed_len, armed_crc;
+    val_batch_stats_t st;
+    uint32_t *crc_tmp;
+    uint64_t *off_tmp;
+    uint32_t *len_tmp;
+};
+
+static val_batch_t *volatile g_reg[VB_MAX_ATTACHED];
+
+static val_batch_t *vb_lookup(const void *buf, int rx)
+{
+    for (int i = 0; i < VB_MAX_ATTACHED; i++) {
+        val_batch_t *b = __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
+        if (b && (rx ? (const void *)b->recv_buffer : (const void *)b->send_buffer) == buf) return b;
+    }
+    return NULL;
+}
+
+static uint32_t vb_direct(val_batch_t *b, uint32_t seed, const void *buf, size_t len)
+{
+    if (b) b->st.direct_answers++;
+    crc32_func_t p = b && b->u_provider ? b->u_provider : val_gpu_crc32_provider;
+    return p(seed, buf, len);
+}
+
+static void vb_fail(val_batch_t *b, val_status_t st)
+{
+    if (b->st.status == VAL_OK) b->st.status = st;
+}
+
+/* CRCs of frames f[0..n) of buf in one host batch call. */
+static val_status_t vb_hash(val_batch_t *b, const uint8_t *buf, size_t used, vb_frame_t *f, uint32_t n, int only_needed)
+{
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (!only_needed || f[i].need) {
+            b->off_tmp[k] = f[i].off;
+            b->len_tmp[k] = f[i].len;
+            k++;
+        }
+    if (!k) return VAL_OK;
+    val_status_t st = val_crc32_frames_host(buf, used, b->off_tmp, b->len_tmp, 0, 0, k, b->crc_tmp, NULL);
+    if (st != VAL_OK) return st;
+    k = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (!only_needed || f[i].need) f[i].crc = b->crc_tmp[k++];
+    return VAL_OK;
+}
+
+/* ---- TX ---------------------------------------------------------------- */
+static val_status_t vb_flush_tx(val_batch_t *b)
+{
+    if (!b->tx_n) return b->st.status;
+    uint32_t need = 0;
+    for (uint32_t i = 0; i < b->tx_n; i++) need += b->txf[i].need;
+    val_status_t st = b->st.status;
+    if (st == VAL_OK && need) {
+        st = vb_hash(b, b->tx, b->tx_used, b->txf, b->tx_n, 1);
+        if (st == VAL_OK) {
+            b->st.tx_batches++;
+            b->st.tx_batched_frames += need;
+            if (need > b->st.tx_max_batch) b->st.tx_max_batch = need;
+            for (uint32_t i = 0; i < b->tx_n; i++)
+                if (b->txf[i].need) {
+                    uint8_t *t = b->tx + b->txf[i].off + b->txf[i].len;
+                    const uint32_t c = b->txf[i].crc;
+                    t[0] = (uint8_t)c;
+                    t[1] = (uint8_t)(c >> 8);
+                    t[2] = (uint8_t)(c >> 16);
+                    t[3] = (uint8_t)(c >> 24);
+                }
+        } else {
+            vb_fail(b, st);
+        }
+    }
+    if (st == VAL_OK) {
+        if (b->opt.coalesce_send) {
+            if (b->u_send(b->u_io, b->tx, b->tx_used) != (int)b->tx_used) vb_fail(b, st = VAL_ERR_IO);
+        } else {
+            for (uint32_t i = 0; i < b->tx_n && st == VAL_OK; i++) {
+                const size_t wl = (size_t)b->txf[i].len + VAL_WIRE_TRAILER_SIZE;
+                if (b->u_send(b->u_io, b->tx + b->txf[i].off, wl) != (int)wl) vb_fail(b, st = VAL_ERR_IO);
+            }
+        }
+        if (st == VAL_OK) b->st.tx_frames += b->tx_n;
+    }
+    b->tx_n = 0;
+    b->tx_used = 0;
+    return st;
+}
+
+static int vb_send(void *ctx, const void *data, size_t len)
+{
+    val_batch_t *b = (val_batch_t *)ctx;
+    const size_t pending = b->tx_pending;
+    b->tx_pending = 0;
+    if (b->st.status != VAL_OK) return -1;
+    if (!b->opt.tx || len < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE || len > b->opt.max_bytes) {
+        /* not a frame this batcher stages: send the window before it, then it */
+        if (vb_flush_tx(b) != VAL_OK) return -1;
+        const int rc = b->u_send(b->u_io, data, len);
+        if (rc == (int)len) b->st.tx_frames++;
+        return rc;
+    }
+    if (b->tx_n == b->opt.max_frames || b->tx_used + len > b->opt.max_bytes)
+        if (vb_flush_tx(b) != VAL_OK) return -1;
+    vb_frame_t *f = &b->txf[b->tx_n++];
+    f->off = b->tx_used;
+    f->len = (uint32_t)(len - VAL_WIRE_TRAILER_SIZE);
+    /* the provider returned a placeholder for exactly this frame */
+    f->need = (uint8_t)(data == (const void *)b->send_buffer && pending == f->len);
+    memcpy(b->tx + b->tx_used, data, len);
+    b->tx_used += len;
+    const uint8_t type = ((const uint8_t *)data)[0];
+    /* only DATA frames wait for the rest of their window: a control frame
+       (ACK, DONE, EOT, ...) goes out at once with everything before it */
+    if (type != VAL_PKT_DATA && vb_flush_tx(b) != VAL_OK) return -1;
+    return (int)len;
+}
+
+static void vb_flush_hook(void *ctx)
+{
+    val_batch_t *b = (val_batch_t *)ctx;
+    (void)vb_flush_tx(b);
+    if (b->u_flush) b->u_flush(b->u_io);
+}
+
+static int vb_is_connected(void *ctx)
+{
+    val_batch_t *b = (val_batch_t *)ctx;
+    return b->u_is_connected ? b->u_is_connected(b->u_io) : 1;
+}
+
+/* ---- RX ---------------------------------------------------------------- */
+/* Read exactly n bytes into dst from the application's transport within
+ * timeout (its recv may return fewer); returns the bytes read or -1. */
+static long vb_read(val_batch_t *b, uint8_t *dst, size_t n, uint32_t timeout_ms)
+{
+    size_t got = 0;
+    const int rc = b->u_recv(b->u_io, dst, n, &got, timeout_ms);
+    if (rc < 0) return -1;
+    return (long)(got > n ? n : got);
+}
+
+static size_t vb_content_max(const val_batch_t *b)
+{
+    return b->mtu - VAL_WIRE_HEADER_SIZE - VAL_WIRE_TRAILER_SIZE;
+}
+
+/* Refill the empty ring: the frame in progress (or the next one, waiting up
+ * to timeout_ms for its first byte), then every further frame the transport
+ * already holds. Complete frames are hashed in one batch. Returns 0, or -1
+ * on a transport error. */
+static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
+{
+    b->r_base += b->r_len;
+    b->r_head = b->r_len = 0;
+    b->rx_n = b->rx_cur = 0;
+    const size_t cap = b->opt.max_bytes;
+    if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
+    int first = 1;
+    for (;;) {
+        if (b->owe == 0) {
+            /* at a frame boundary: the next header */
+            if (b->rx_n >= b->opt.max_frames || cap - b->r_len < b->mtu) break;
+            const uint32_t t = first ? timeout_ms : 0u;
+            long g = vb_read(b, b->hdr_part + b->hdr_have, VAL_WIRE_HEADER_SIZE - b->hdr_have, t);
+            if (g < 0) return -1;
+            if (g == 0 && b->hdr_have == 0) break;
+            const size_t start_have = b->hdr_have;
+            b->hdr_have += (size_t)g;
+            if (b->hdr_have < VAL_WIRE_HEADER_SIZE) {
+                /* a partial header: the rest is owed (deliver what we have) */
+                memcpy(b->rx + b->r_len, b->hdr_part + start_have, (size_t)g);
+                b->r_len += (size_t)g;
+                break;
+            }
+            const size_t content = (size_t)b->hdr_part[2] | (size_t)b->hdr_part[3] << 8;
+            memcpy(b->rx + b->r_len, b->hdr_part + start_have, VAL_WIRE_HEADER_SIZE - start_have);
+            const uint64_t fstart = b->r_len - start_have;  /* may lie before this ring (partial header) */
+            b->r_len += VAL_WIRE_HEADER_SIZE - start_have;
+            b->hdr_have = 0;
+            if (content > vb_content_max(b)) {
+                /* the session will reject it (src/val_core.c:915-921); the
+                   stream has no trustworthy boundaries after this */
+                b->raw = 1;
+                break;
+            }
+            b->owe = content + VAL_WIRE_TRAILER_SIZE;
+            const long r = vb_read(b, b->rx + b->r_len, b->owe, timeout_ms);
+            if (r < 0) return -1;
+            b->r_len += (size_t)r;
+            b->owe -= (size_t)r;
+            if (b->owe) break;  /* the rest is late: stop reading ahead */
+            if (start_have == 0) {
+                vb_frame_t *f = &b->rxf[b->rx_n++];
+                f->off = fstart;
+                f->len = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
+                f->need = 1;
+            }
+            first = 0;
+        } else {
+            /* the rest of a frame that began in the previous ring */
+            const long r = vb_read(b, b->rx + b->r_len, b->owe, timeout_ms);
+            if (r < 0) return -1;
+            b->r_len += (size_t)r;
+            b->owe -= (size_t)r;
+            if (b->owe || r == 0) break;
+            first = 0;
+        }
+    }
+    if (b->rx_n) {
+        const val_status_t st = vb_hash(b, b->rx, b->r_len, b->rxf, b->rx_n, 0);
+        if (st != VAL_OK) {
+            vb_fail(b, st);
+            b->rx_n = 0;  /* the session's checks are then computed directly */
+        } else {
+            b->st.rx_batches++;
+            b->st.rx_frames += b->rx_n;
+            if (b->rx_n > b->st.rx_max_batch) b->st.rx_max_batch = b->rx_n;
+        }
+    }
+    return 0;
+}
+
+/* Bytes [pos, pos + n) of the ring went to dst: track whether frame rx_cur
+ * is being delivered to recv_buffer in place, and arm its CRC for the
+ * provider call that follows its trailer. */
+static void vb_track(val_batch_t *b, size_t pos, size_t n, const uint8_t *dst)
+{
+    b->armed = 0;
+    while (n && b->rx_cur < b->rx_n) {
+        vb_frame_t *f = &b->rxf[b->rx_cur];
+        const size_t fs = (size_t)f->off, fe = fs + f->len + VAL_WIRE_TRAILER_SIZE;
+        if (pos >= fe) {
+            b->rx_cur++;
+            b->cur_matched = 0;
+            continue;
+        }
+        if (pos < fs) {  /* bytes before this frame (a partial tail of an earlier one) */
+            const size_t skip = fs - pos < n ? fs - pos : n;
+            pos += skip;
+            dst += skip;
+            n -= skip;
+            continue;
+        }
+        const size_t take = fe - pos < n ? fe - pos : n;
+        /* CRC-input bytes of this piece that landed at recv_buffer + (pos - fs) */
+        const size_t ce = fs + f->len;
+        if (pos < ce) {
+            const size_t cn = (ce - pos < take) ? ce - pos : take;
+            if (dst == b->recv_buffer + (pos - fs)) b->cur_matched += cn;
+        }
+        pos += take;
+        dst += take;
+        n -= take;
+        if (pos == fe) {
+            if (b->cur_matched == f->len) {
+                b->armed = 1;
+                b->armed_len = f->len;
+                b->armed_crc = f->crc;
+            }
+            b->rx_cur++;
+            b->cur_matched = 0;
+        }
+    }
+}
+
+static int vb_recv(void *ctx, void *buffer, size_t size, size_t *received, uint32_t timeout_ms)
+{
+    val_batch_t *b = (val_batch_t *)ctx;
+    if (received) *received = 0;
+    /* the session is about to wait: its staged window goes out first */
+    if (vb_flush_tx(b) != VAL_OK) return -1;
+    if (!b->opt.rx) return b->u_recv(b->u_io, buffer, size, received, timeout_ms);
+    if (b->r_head == b->r_len) {
+        if (b->raw) {
+            b->armed = 0;
+            return b->u_recv(b->u_io, buffer, size, received, timeout_ms);
+        }
+        if (vb_fill(b, timeout_ms) < 0) return -1;
+    }
+    size_t n = b->r_len - b->r_head;
+    if (n > size) n = size;
+    if (n) {
+        memcpy(buffer, b->rx + b->r_head, n);
+        vb_track(b, b->r_head, n, (const uint8_t *)buffer);
+        b->r_head += n;
+    }
+    if (received) *received = n;
+    return 0;
+}
+
+/* ---- the provider ------------------------------------------------------ */
+uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
+{
+    val_batch_t *b = vb_lookup(buf, 0);
+    if (b) {
+        if (b->opt.tx && seed == 0xFFFFFFFFu && b->st.status == VAL_OK) {
+            /* a TX frame in send_buffer: its trailer comes from the window batch */
+            b->tx_pending = len;
+            return 0u;
+        }
+        return vb_direct(b, seed, buf, len);
+    }
+    b = vb_lookup(buf, 1);
+    if (b && b->armed && seed == 0xFFFFFFFFu && len == b->armed_len) {
+        b->armed = 0;
+        b->st.rx_batched_answers++;
+        return b->armed_crc;
+    }
+    return vb_direct(b, seed, buf, len);
+}
+
+/* ---- lifetime ---------------------------------------------------------- */
+static void *vb_alloc(val_batch_t *b, size_t n)
+{
+    void *p = b->pinned ? val_gpu_host_alloc(n) : NULL;
+    if (!p) {
+        b->pinned = 0;
+        p = malloc(n);
+    }
+    return p;
+}
+
+static void vb_free(val_batch_t *b, void *p)
+{
+    if (!p) return;
+    if (b->pinned) val_gpu_host_free(p);
+    else free(p);
+}
+
+val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out)
+{
+    if (!cfg || !out || !cfg->transport.send || !cfg->transport.recv || !cfg->buffers.send_buffer ||
+        !cfg->buffers.recv_buffer || cfg->buffers.packet_size < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE)
+        return VAL_ERR_INVALID_ARG;
+    val_batch_t *b = (val_batch_t *)calloc(1, sizeof *b);
+    if (!b) return VAL_ERR_NO_MEMORY;
+    if (opts) b->opt = *opts;
+    else {
+        b->opt.tx = 1;
+        b->opt.rx = 1;
+    }
+    if (!b->opt.max_frames) b->opt.max_frames = VB_DEFAULT_FRAMES;
+    if (!b->opt.max_bytes) b->opt.max_bytes = VB_DEFAULT_BYTES;
+    b->mtu = cfg->buffers.packet_size;
+    if (b->opt.max_bytes < b->mtu) b->opt.max_bytes = b->mtu;
+    b->cfg = cfg;
+    b->u_send = cfg->transport.send;
+    b->u_recv = cfg->transport.recv;
+    b->u_is_connected = cfg->transport.is_connected;
+    b->u_flush = cfg->transport.flush;
+    b->u_io = cfg->transport.io_context;
+    b->u_provider = cfg->crc32_provider;
+    b->send_buffer = (const uint8_t *)cfg->buffers.send_buffer;
+    b->recv_buffer = (const uint8_t *)cfg->buffers.recv_buffer;
+    b->pinned = val_gpu_device_count() > 0;  /* pinned windows: DMA in place on the GPU path */
+    const uint32_t nf = b->opt.max_frames;
+    b->tx = (uint8_t *)vb_alloc(b, b->opt.max_bytes);
+    b->rx = (uint8_t *)vb_alloc(b, b->opt.max_bytes);
+    b->txf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
+    b->rxf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
+    b->crc_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
+    b->off_tmp = (uint64_t *)calloc(nf, sizeof(uint64_t));
+    b->len_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
+    int slot = -1;
+    for (int i = 0; i < VB_MAX_ATTACHED && slot < 0; i++) {
+        val_batch_t *expect = NULL;
+        if (__atomic_compare_exchange_n(&g_reg[i], &expect, b, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) slot = i;
+    }
+    if (!b->tx || !b->rx || !b->txf || !b->rxf || !b->crc_tmp || !b->off_tmp || !b->len_tmp || slot < 0) {
+        if (slot >= 0) __atomic_store_n(&g_reg[slot], NULL, __ATOMIC_RELEASE);
+        vb_free(b, b->tx);
+        vb_free(b, b->rx);
+        free(b->txf);
+        free(b->rxf);
+        free(b->crc_tmp);
+        free(b->off_tmp);
+        free(b->len_tmp);
+        free(b);
+        return slot < 0 ? VAL_ERR_INVALID_ARG : VAL_ERR_NO_MEMORY;
+    }
+    b->st.status = VAL_OK;
+    cfg->transport.send = vb_send;
+    cfg->transport.recv = vb_recv;
+    cfg->transport.is_connected = b->u_is_connected ? vb_is_connected : NULL;
+    cfg->transport.flush = vb_flush_hook;
+    cfg->transport.io_context = b;
+    cfg->crc32_provider = val_batch_crc32_provider;
+    *out = b;
+    return VAL_OK;
+}
+
+val_status_t val_batch_flush(val_batch_t *b)
+{
+    return b ? vb_flush_tx(b) : VAL_ERR_INVALID_ARG;
+}
+
+void val_batch_get_stats(const val_batch_t *b, val_batch_stats_t *out)
+{
+    if (!out) return;
+    if (!b) {
+        memset(out, 0, sizeof *out);
+        return;
+    }
+    *out = b->st;
+}
+
+void val_batch_detach(val_batch_t *b)
+{
+    if (!b) return;
+    (void)vb_flush_tx(b);
+    for (int i = 0; i < VB_MAX_ATTACHED; i++) {
+        val_batch_t *expect = b;
+        if (__atomic_compare_exchange_n(&g_reg[i], &expect, NULL, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) break;
+    }
+    val_config_t *cfg = b->cfg;
+    cfg->transport.send = b->u_send;
+    cfg->transport.recv = b->u_recv;
+    cfg->transport.is_connected = b->u_is_connected;
+    cfg->transport.flush = b->u_flush;
+    cfg->transport.io_context = b->u_io;
+    cfg->crc32_provider = b->u_provider;
+    vb_free(b, b->tx);
+    vb_free(b, b->rx);
+    free(b->txf);
+    free(b->rxf);
+    free(b->crc_tmp);
+    free(b->off_tmp);
+    free(b->len_tmp);
+    free(b);
+}

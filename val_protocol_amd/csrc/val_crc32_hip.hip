@@ -60,6 +60,11 @@ struct StreamScratch {
     // used by a launch while its stream was capturing a graph: the graph may
     // replay at any time, so the scratch is never evicted
     bool captured = false;
+    // a kernel used the scratch without binding `done` (the binning launches
+    // before a tracked launch that then failed, or a launch whose capture
+    // status could not be queried): not drainable until the next successful
+    // tracked launch on the stream, which completes after it
+    bool untracked = false;
     Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin;     // ragged binning: counts, plan, sorted order
     Arena queue;   // k_frames dynamic tail {head, exits} (zero between calls)
@@ -565,7 +570,7 @@ void scratch_free(StreamScratch *x)
 // failed; the caller then evicts another entry.
 bool scratch_drain(StreamScratch *x)
 {
-    if (x->captured || !x->done) return false;
+    if (x->captured || x->untracked || !x->done) return false;
     if (hipEventSynchronize(x->done) != hipSuccess) {
         (void)hipGetLastError();
         return false;
@@ -609,21 +614,28 @@ StreamScratch &scratch_for(Ctx &c, hipStream_t s)
 
 // Launch a kernel that uses x's scratch, binding x's completion event to the
 // dispatch. While s is capturing a graph the kernel is launched plainly and
-// the entry is kept for good (the graph owns that use of the scratch).
+// the entry is kept for good (the graph owns that use of the scratch). When
+// the capture status cannot be queried (e.g. the legacy stream while another
+// stream captures) the launch is plain and the entry is held only until the
+// next tracked launch succeeds; a failed tracked launch holds it the same way.
 template <typename K, typename... Args>
 hipError_t launch_tracked(StreamScratch *x, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args)
 {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    bool unknown = false;
     if (x && hipStreamIsCapturing(s, &cap) != hipSuccess) {
         (void)hipGetLastError();
-        cap = hipStreamCaptureStatusActive;  // unknown: treat as captured
+        unknown = true;
     }
-    if (x && cap == hipStreamCaptureStatusNone && x->done) {
+    if (x && !unknown && cap == hipStreamCaptureStatusNone && x->done) {
         hipExtLaunchKernelGGL(kernel, grid, block, 0, s, nullptr, x->done, 0u, args...);
-    } else {
-        if (x) x->captured = true;
-        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+        const hipError_t e = hipGetLastError();
+        x->untracked = e != hipSuccess;  // on failure `done` names an older dispatch
+        return e;
     }
+    if (x && unknown) x->untracked = true;
+    else if (x) x->captured = true;
+    hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
     return hipGetLastError();
 }
 
@@ -680,6 +692,7 @@ val_status_t launch_ragged(Ctx &c, FrameParams &p, hipStream_t s)
     hipError_t e = a.counts_zero ? hipSuccess : hipMemsetAsync(gcount, 0, sz_gcount, s);
     a.counts_zero = false;
     if (e == hipSuccess) {
+        ss.untracked = true;  // the binning launches are not bound to `done`; the tracked launch clears it
         hipLaunchKernelGGL(k_bin_count, dim3(nbin), dim3(kBinThreads), 0, s, p.len, n, chunk, gcount, blockoff);
         hipLaunchKernelGGL(k_bin_scatter, dim3(nbin), dim3(kBinThreads), 0, s, p.len, n, chunk, gcount, blockoff, ctab,
                            heads, order);
@@ -857,12 +870,40 @@ bool is_pinned(const void *p)
 // MiB. Concurrent copies (one per device in the *_host_multi calls) share
 // the process's CPU affinity set: the threads of all copies in flight never
 // exceed it (8 devices x 8 threads would be 64 threads on a 16-core share).
+// The budget is the affinity set capped by the cgroup CPU quota: a GPU box
+// shows every CPU of the machine in the affinity set (256) but its quota pays
+// for one GPU's share (16).
+unsigned cgroup_cpu_quota()
+{
+    unsigned q = 0;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota> <period>" or "max <period>"
+        char a[32] = {0};
+        double per = 0;
+        if (fscanf(f, "%31s %lf", a, &per) == 2 && strcmp(a, "max") != 0 && per > 0) {
+            const double v = atof(a) / per;
+            if (v > 0) q = (unsigned)std::max(1.0, v + 0.999);
+        }
+        fclose(f);
+        return q;
+    }
+    FILE *fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r");  // cgroup v1
+    FILE *fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r");
+    double quota = -1, per = 0;
+    if (fq && fp && fscanf(fq, "%lf", &quota) == 1 && fscanf(fp, "%lf", &per) == 1 && quota > 0 && per > 0)
+        q = (unsigned)std::max(1.0, quota / per + 0.999);
+    if (fq) fclose(fq);
+    if (fp) fclose(fp);
+    return q;
+}
+
 unsigned host_cpu_budget()
 {
     static const unsigned n = [] {
+        unsigned a = std::max(1u, std::thread::hardware_concurrency());
         cpu_set_t set;
-        if (sched_getaffinity(0, sizeof set, &set) == 0) return (unsigned)std::max(1, CPU_COUNT(&set));
-        return std::max(1u, std::thread::hardware_concurrency());
+        if (sched_getaffinity(0, sizeof set, &set) == 0) a = (unsigned)std::max(1, CPU_COUNT(&set));
+        const unsigned q = cgroup_cpu_quota();
+        return q ? std::min(a, q) : a;
     }();
     return n;
 }
@@ -887,7 +928,12 @@ void parallel_copy(uint8_t *dst, const uint8_t *src, size_t n)
         const size_t per = (n + nt - 1) / nt;
         for (size_t t = 1; t < nt; t++) {
             const size_t lo = t * per, hi = std::min(n, lo + per);
-            if (lo < hi) th.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
+            if (lo >= hi) continue;
+            try {
+                th.emplace_back([=] { memcpy(dst + lo, src + lo, hi - lo); });
+            } catch (...) {  // no thread: the calling thread copies this piece
+                memcpy(dst + lo, src + lo, hi - lo);
+            }
         }
         memcpy(dst, src, std::min(n, per));  // the calling thread takes the first piece
         for (auto &x : th) x.join();
@@ -1182,23 +1228,36 @@ uint32_t cpu_frames_range(const uint8_t *base, const uint64_t *off, const uint32
 // The whole batch on the calling thread plus helper threads (contiguous
 // frame ranges balanced by bytes, as the multi-GPU split).
 // Helper threads only for batches of at least 4 MiB per thread: a thread
-// start costs more than a small window's whole CRC.
+// start costs more than a small window's whole CRC. The thread count is
+// val_gpu_set_host_cpu_threads capped by the process's CPU budget (affinity
+// and cgroup quota). A helper thread that cannot be started leaves its range
+// to the calling thread (the C entry points must not throw).
 uint32_t cpu_frames(const uint8_t *base, const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t flen,
                     uint32_t n, uint64_t total, int verify, uint32_t *crc, uint32_t *hdr, uint8_t *ok, uint32_t *pay)
 {
     g_cpu_batches.fetch_add(1, std::memory_order_relaxed);
     const uint64_t by_size = std::max<uint64_t>(1, total >> 22);
     const uint32_t nt = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>({(uint64_t)g_host_cpu_threads.load(), by_size, (uint64_t)std::max(n, 1u)}));
+        1, std::min<uint64_t>({(uint64_t)g_host_cpu_threads.load(), (uint64_t)host_cpu_budget(), by_size,
+                               (uint64_t)std::max(n, 1u)}));
     if (nt == 1) return cpu_frames_range(base, off, len, stride, flen, 0, n, verify, crc, hdr, ok, pay);
     const std::vector<uint32_t> cut = shard_cuts(n, len, nt);
     std::vector<uint32_t> bad(nt, 0);
     std::vector<std::thread> th;
-    for (uint32_t t = 1; t < nt; t++)
-        th.emplace_back([&, t] {
-            bad[t] = cpu_frames_range(base, off, len, stride, flen, cut[t], cut[t + 1], verify, crc, hdr, ok, pay);
-        });
+    uint32_t started = 1;  // ranges [1, started) run on helper threads
+    for (; started < nt; started++) {
+        const uint32_t t = started;
+        try {
+            th.emplace_back([&, t] {
+                bad[t] = cpu_frames_range(base, off, len, stride, flen, cut[t], cut[t + 1], verify, crc, hdr, ok, pay);
+            });
+        } catch (...) {
+            break;
+        }
+    }
     bad[0] = cpu_frames_range(base, off, len, stride, flen, cut[0], cut[1], verify, crc, hdr, ok, pay);
+    for (uint32_t t = started; t < nt; t++)
+        bad[t] = cpu_frames_range(base, off, len, stride, flen, cut[t], cut[t + 1], verify, crc, hdr, ok, pay);
     for (auto &x : th) x.join();
     uint32_t nbad = 0;
     for (uint32_t b : bad) nbad += b;
@@ -1211,9 +1270,11 @@ uint32_t cpu_frames(const uint8_t *base, const uint64_t *off, const uint32_t *le
 // chunk c-1's kernel on the compute stream; the outputs come back D2H once at
 // the end. Descriptor batches are chunked when their offsets are
 // non-decreasing (a packed stream); otherwise the whole span is one chunk.
+// route_cpu == false: the caller (frames_host_multi) already chose the GPU for
+// the whole batch, so this shard skips the single-GPU crossover.
 val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                          uint64_t stride, uint32_t flen, uint32_t n, int verify, uint32_t *crc, uint32_t *hdr,
-                         uint8_t *ok, uint32_t *nbad, uint32_t *pay = nullptr)
+                         uint8_t *ok, uint32_t *nbad, uint32_t *pay = nullptr, bool route_cpu = true)
 {
     if (!base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
     if ((off == nullptr) != (len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
@@ -1230,7 +1291,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         total += l;
         if (off && i && off[i] < off[i - 1]) monotone = false;
     }
-    if (total < host_batch_min_bytes()) {  // below the crossover: the CPU engine (no device needed)
+    if (route_cpu && total < host_batch_min_bytes()) {  // below the crossover: the CPU engine (no device needed)
         const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, pay);
         if (nbad) *nbad = verify ? bad : 0u;
         return VAL_OK;
@@ -1401,35 +1462,86 @@ void shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t rank
     *count = cut[rank + 1] - cut[rank];
 }
 
+// CPU or GPU for a whole host batch over `devices` distinct GPUs (the
+// *_host_multi calls decide once, never per shard). The single-GPU crossover
+// C1 (host_batch_min_bytes) was measured against one CPU thread. With N
+// devices each shard's H2D runs on its own PCIe link and DMA engines while
+// the fixed costs (launch, completion wait, first chunk) are paid
+// concurrently, so the GPU side's byte rate scales with N; the CPU engine's
+// scales with its T threads (val_gpu_set_host_cpu_threads, capped by the
+// CPU budget). First-order crossover: C(N, T) = C1 * T / N (DESIGN.md
+// section 1). A GPU test that forces C1 = 0 keeps every batch on the GPU.
+uint64_t host_multi_min_bytes(int devices)
+{
+    const uint64_t t = std::max<uint64_t>(1, std::min<uint64_t>(g_host_cpu_threads.load(), host_cpu_budget()));
+    return host_batch_min_bytes() * t / (uint64_t)std::max(1, devices);
+}
+
+// Run work(0..k-1): k-1 helper threads plus the calling thread; a helper that
+// cannot be started leaves its index to the calling thread.
+template <typename F>
+void run_shards(int k, F &&work)
+{
+    std::vector<std::thread> th;
+    int started = 1;
+    for (; started < k; started++) {
+        try {
+            th.emplace_back(work, started);
+        } catch (...) {
+            break;
+        }
+    }
+    work(0);
+    for (int d = started; d < k; d++) work(d);
+    for (auto &x : th) x.join();
+}
+
 val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uint64_t *off, const uint32_t *len,
                                uint64_t stride, uint32_t flen, uint32_t n, int verify, uint32_t *crc, uint32_t *hdr,
                                uint8_t *ok, uint32_t *nbad, int ndev)
 {
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(VAL_ERR_IO, "no HIP device");
-    if (ndev <= 0) ndev = std::min(count, kMaxDevices);
-    ndev = std::min(ndev, kMaxDevices);
+    if (!base && n) return fail(VAL_ERR_INVALID_ARG, "base is NULL");
     if ((off == nullptr) != (len == nullptr)) return fail(VAL_ERR_INVALID_ARG, "off/len must both be set or both NULL");
+    const uint64_t tail = verify ? 4u : 0u;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t o = off ? off[i] : (uint64_t)i * stride;
+        const uint64_t l = len ? len[i] : flen;
+        if (o > base_len || l + tail > base_len - o) return fail(VAL_ERR_INVALID_ARG, "frame overruns the buffer");
+        total += l;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 0) {
+        (void)hipGetLastError();
+        count = 0;
+    }
+    if (ndev <= 0) ndev = std::max(1, std::min(count, kMaxDevices));
+    ndev = std::min(ndev, kMaxDevices);
+    // one decision for the whole batch: distinct devices the shards land on
+    if (total < host_multi_min_bytes(std::max(1, std::min(ndev, count)))) {
+        const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, nullptr);
+        if (nbad) *nbad = verify ? bad : 0u;
+        return VAL_OK;
+    }
+    if (count <= 0) return fail(VAL_ERR_IO, "no HIP device");
     std::vector<val_status_t> st(ndev, VAL_OK);
     std::vector<uint32_t> bad(ndev, 0);
     std::vector<std::string> err(ndev);
     const std::vector<uint32_t> cut = shard_cuts(n, len, (uint32_t)ndev);
     auto work = [&](int d) {
+        const int prev = t_dev;
         t_dev = d % count;  // more shards than devices share them round-robin
         const uint32_t s0 = cut[d], cnt = cut[d + 1] - cut[d];
         const bool strided = off == nullptr;
         const uint8_t *b = strided ? base + (uint64_t)s0 * stride : base;
         const uint64_t bl = strided ? base_len - std::min<uint64_t>(base_len, (uint64_t)s0 * stride) : base_len;
         st[d] = frames_host(b, bl, strided ? nullptr : off + s0, strided ? nullptr : len + s0, stride, flen, cnt, verify,
-                            crc ? crc + s0 : nullptr, hdr ? hdr + s0 : nullptr, ok ? ok + s0 : nullptr, &bad[d]);
+                            crc ? crc + s0 : nullptr, hdr ? hdr + s0 : nullptr, ok ? ok + s0 : nullptr, &bad[d],
+                            nullptr, /*route_cpu=*/false);
         err[d] = t_err;
+        t_dev = prev;
     };
-    const int saved = t_dev;
-    std::vector<std::thread> th;
-    for (int d = 1; d < ndev; d++) th.emplace_back(work, d);
-    work(0);
-    for (auto &x : th) x.join();
-    t_dev = saved;
+    run_shards(ndev, work);
     uint32_t total_bad = 0;
     for (int d = 0; d < ndev; d++) {
         if (st[d] != VAL_OK) {
@@ -1444,33 +1556,49 @@ val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uin
 
 // One long host window split into byte ranges, one per device (4 KiB
 // aligned); device 0's range starts from state_in, the others from 0; the
-// partial raw states fold in order with the GF(2) shift.
+// partial raw states fold in order with the GF(2) shift. Below the N-device
+// crossover (host_multi_min_bytes, decided once for the whole window) the CPU
+// engine folds the window on the calling thread plus helper threads (>= 4 MiB
+// each, within the CPU budget), the same way.
 val_status_t region_host_multi(const void *data, uint64_t len, uint32_t state_in, uint32_t *state_out, int ndev)
 {
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(VAL_ERR_IO, "no HIP device");
-    if (ndev <= 0) ndev = std::min(count, kMaxDevices);
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 0) {
+        (void)hipGetLastError();
+        count = 0;
+    }
+    if (ndev <= 0) ndev = std::max(1, std::min(count, kMaxDevices));
     ndev = std::min(ndev, kMaxDevices);
-    const uint64_t per = ((len + ndev - 1) / ndev + 4095u) & ~(uint64_t)4095u;
-    std::vector<val_status_t> st(ndev, VAL_OK);
-    std::vector<uint32_t> part(ndev, 0);
-    std::vector<uint64_t> plen(ndev, 0);
-    std::vector<std::string> err(ndev);
+    const bool on_cpu = len < host_multi_min_bytes(std::max(1, std::min(ndev, count)));
+    if (!on_cpu && count <= 0) return fail(VAL_ERR_IO, "no HIP device");
+    int parts = ndev;
+    if (on_cpu) {
+        g_cpu_batches.fetch_add(1, std::memory_order_relaxed);
+        parts = (int)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)g_host_cpu_threads.load(),
+                                                               (uint64_t)host_cpu_budget(), len >> 22}));
+    }
+    const uint64_t per = ((len + parts - 1) / parts + 4095u) & ~(uint64_t)4095u;
+    std::vector<val_status_t> st(parts, VAL_OK);
+    std::vector<uint32_t> part(parts, 0);
+    std::vector<uint64_t> plen(parts, 0);
+    std::vector<std::string> err(parts);
     auto work = [&](int d) {
-        t_dev = d % count;  // more shards than devices share them round-robin
         const uint64_t lo = std::min(len, (uint64_t)d * per), hi = std::min(len, lo + per);
+        const uint8_t *p = static_cast<const uint8_t *>(data) + lo;
         plen[d] = hi - lo;
-        st[d] = region_host(static_cast<const uint8_t *>(data) + lo, (size_t)(hi - lo), d == 0 ? state_in : 0u, &part[d]);
+        if (on_cpu) {
+            part[d] = vcrc_cpu_update(d == 0 ? state_in : 0u, p, (size_t)(hi - lo));
+            return;
+        }
+        const int prev = t_dev;
+        t_dev = d % count;  // more shards than devices share them round-robin
+        st[d] = region_host(p, (size_t)(hi - lo), d == 0 ? state_in : 0u, &part[d]);
         err[d] = t_err;
+        t_dev = prev;
     };
-    const int saved = t_dev;
-    std::vector<std::thread> th;
-    for (int d = 1; d < ndev; d++) th.emplace_back(work, d);
-    work(0);
-    for (auto &x : th) x.join();
-    t_dev = saved;
+    run_shards(parts, work);
     uint32_t acc = 0;
-    for (int d = 0; d < ndev; d++) {
+    for (int d = 0; d < parts; d++) {
         if (st[d] != VAL_OK) {
             t_err = "device " + std::to_string(d) + ": " + err[d];
             return st[d];
@@ -1704,6 +1832,8 @@ void val_gpu_set_host_cpu_threads(uint32_t threads)
 {
     g_host_cpu_threads.store(std::max<uint32_t>(1, std::min<uint32_t>(threads, 256)));
 }
+
+uint64_t val_gpu_host_multi_min_bytes(int devices) { return host_multi_min_bytes(devices); }
 
 void val_gpu_set_ragged_min_frames(int64_t frames) { g_ragged_min.store(frames < 0 ? -1 : frames); }
 
