@@ -79,6 +79,28 @@ def test_region_host_multi(vc, ndev, length):
     assert got == _oracle.crc32(data)
 
 
+def test_multi_at_default_thresholds_reaches_the_gpu(vc):
+    """At the library's built-in crossover (64 MiB for one GPU and one CPU
+    thread; the suite normally forces 0) a 256 MiB batch split over ndev = 8
+    shards is decided once for the whole batch, goes to the GPU (the CPU
+    counter does not move; each 32 MiB shard alone is below the single-GPU
+    crossover and used to be answered on the CPU) and is bit-exact."""
+    vc.set_host_batch_min_bytes(64 << 20)
+    try:
+        n, flen, stride = 16384, 16400, 16404  # 268.7 MB of CRC input
+        sb = _prng.prng_bytes(0x256, n * stride)
+        want = _oracle.frames_strided(sb, stride, flen, n, nthreads=8)
+        before = vc.cpu_batch_count()
+        for ndev in (8, 0):
+            assert np.array_equal(vc.frames_host_multi(sb, stride=stride, flen=flen, n=n, ndev=ndev), want)
+        data = sb[: 200 << 20]
+        assert vc.region_host_multi(data, 0xFFFFFFFF, ndev=8) ^ 0xFFFFFFFF == _oracle.crc32(data)
+        assert vc.cpu_batch_count() == before
+        assert vc.host_multi_min_bytes(vc.device_count()) <= 64 << 20
+    finally:
+        vc.set_host_batch_min_bytes(-1)
+
+
 def test_scalar_hooks_from_many_threads(vc):
     """The provider is called from several sessions' threads at once
     (reference include/val_protocol.h:231-233): reentrant, every CRC exact."""
