@@ -179,8 +179,10 @@ val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len
  * host batch on the GPU pays a launch, a completion wait and PCIe for every
  * byte, and below the measured crossover one CPU core
  * is faster. -1 = VAL_GPU_HOST_BATCH_MIN_BYTES from the environment (read
- * once), else the built-in default; 0 = always the GPU. Such batches need no
- * device and are counted by val_gpu_cpu_batch_count. */
+ * once), else the built-in default, which depends on the batch's mean CRC
+ * input per frame: 64 MiB from 4 KiB frames up, 32 MiB below (the getter
+ * reports the former); 0 = always the GPU. Such batches need no device and
+ * are counted by val_gpu_cpu_batch_count. */
 void val_gpu_set_host_batch_min_bytes(int64_t bytes);
 uint64_t val_gpu_host_batch_min_bytes(void);
 uint64_t val_gpu_cpu_batch_count(void);

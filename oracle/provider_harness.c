@@ -154,7 +154,18 @@ typedef struct {
     frame_rec_t *log;  /* optional frame log (fixtures mode): one record per transport.send */
     size_t nlog, caplog;
     unsigned long recvs;  /* transport.recv calls of this end: frames sent between two are one window fill */
+    unsigned long flip_every, data_sent, flipped;  /* fault injection: one payload bit of every Nth DATA frame */
 } end_t;
+
+/* VAL_HARNESS_FLIP_EVERY=N: the sender's pipe flips one payload bit of every
+ * Nth DATA frame it carries (after logging it), as the reference's own fault
+ * injection does (unit_tests/support/test_support.c:488-503); the receiver
+ * must count a crc_error for each and the transfer still complete. */
+static unsigned long flip_every_env(void)
+{
+    const char *e = getenv("VAL_HARNESS_FLIP_EVERY");
+    return e ? strtoul(e, NULL, 0) : 0ul;
+}
 
 static int tp_send(void *ctx, const void *data, size_t len)
 {
@@ -171,6 +182,16 @@ static int tp_send(void *ctx, const void *data, size_t len)
         memcpy(r->bytes, data, len);
         r->len = len;
         r->epoch = e->recvs;
+    }
+    if (e->flip_every && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA &&
+        ++e->data_sent % e->flip_every == 0) {
+        uint8_t *c = (uint8_t *)malloc(len);
+        memcpy(c, data, len);
+        c[16 + (e->data_sent * 7u) % (len - 20)] ^= 0x10;  /* a payload byte: header and trailer intact */
+        e->flipped++;
+        const int rc = pipe_push(e->out, c, len);
+        free(c);
+        return rc;
     }
     return pipe_push(e->out, (const uint8_t *)data, len);
 }
@@ -672,6 +693,7 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window,
     etx.caplog = erx.caplog = 4096;
     etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
     erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
+    etx.flip_every = flip_every_env();
     crc32_func_t prov = use_gpu ? counting_provider : NULL;
     val_config_t ctx_, crx;
     make_cfg(&ctx_, &etx, mtu, prov);
@@ -711,11 +733,11 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window,
     printf("{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
            "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
-           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"flipped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
            "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
            use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
            mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
-           trailers_ok(&etx) + trailers_ok(&erx), g_calls, t1 - t0,
+           trailers_ok(&etx) + trailers_ok(&erx), etx.flipped, g_calls, t1 - t0,
            (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
            (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
            (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));

@@ -149,3 +149,38 @@ def test_recorded_sessions_with_product(gpu, mode):
             assert tx["tx_max_batch"] > 1 and rx["rx_batched_answers"] > 0, s["name"]
         if s["name"].startswith("window64"):
             assert max(len(w[0]) for w in _sessions.windows(s)) == 64
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
+def test_corrupted_frames_detected_like_the_reference(gpu):
+    """Fault injection as in the reference's own recovery tests
+    (unit_tests/support/test_support.c:488-503; ut_metrics_crc): the
+    sender's pipe flips one payload bit in every 50th DATA frame. With the
+    product installed, plain and batched, the receiver must reject each
+    corrupted frame (crc_errors == frames flipped, src/val_core.c:965-974),
+    and the transfer must proceed exactly as the reference's: at window 1
+    the same retransmissions and the same wire digests; at window 8 the same
+    error count and outcome (the reference's windowed recovery is not ours
+    to fix: whatever it does with its built-in CRC, the product must do)."""
+    env = dict(VAL_HARNESS_FLIP_EVERY="50")
+    os.environ.update(env)
+    try:
+        ref = _line(_run(["none", "loopback", 1 << 20, 1024], gpu))
+        assert ref["flipped"] > 10 and ref["rx_crc_errors"] == ref["flipped"] and ref["equal"] == 1
+        for mode in (["loopback", 1 << 20, 1024], ["loopback-batched", 1 << 20, 1024, 0]):
+            got = _line(_run([vc.LIB_PATH] + mode, gpu))
+            for k in ("tx_status", "rx_status", "equal", "rx_crc_errors", "retransmits", "flipped", "tx_digest",
+                      "rx_digest", "tx_frames", "rx_frames"):
+                assert got[k] == ref[k], (mode[0], k, got[k], ref[k])
+            _lib_counters_clean(got, gpu)
+        ref8 = _line(_run(["none", "loopback", 1 << 20, 1024, 8], gpu))
+        got8 = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, 1024, 8], gpu))
+        for k in ("tx_status", "rx_status", "equal", "flipped"):
+            assert got8[k] == ref8[k], (k, got8[k], ref8[k])
+        assert got8["rx_crc_errors"] == got8["flipped"] == ref8["rx_crc_errors"]
+        assert got8["batch"][0]["tx_max_batch"] == 8
+        _lib_counters_clean(got8, gpu)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)

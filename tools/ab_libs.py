@@ -11,13 +11,28 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import val_protocol_amd.crc as vc  # noqa: E402
-from tools.sweep_geometry import time_it  # noqa: E402
 
 
 def load(path):
     l = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
     vc._declare(l, strict=False)
     return l
+
+
+def time_it(fn, reps=10):
+    """(median, min) ms of fn on the current stream, one event pair per call."""
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts)), float(np.min(ts))
 
 
 def workload(name, dev):

@@ -6,7 +6,9 @@ input) against the library's CPU engine on 1 thread and on the process's
 effective CPU count (threshold 2^62, val_gpu_set_host_cpu_threads), every
 output checked equal. Prints one JSON line per (MTU, W) and a summary line
 with the smallest window where the GPU path beats one CPU thread.
-usage: host_crossover.py [max_bytes]"""
+usage: host_crossover.py [max_bytes] [--fine]
+--fine: windows of 16, 24, ..., 72 MiB of CRC input at each MTU (the band
+where the crossover lies), instead of W = 16 .. 65,535 frames."""
 import json
 import os
 import sys
@@ -31,14 +33,18 @@ def t_call(fn, budget_s=0.4, max_reps=200):
 
 
 def main():
-    max_bytes = int(sys.argv[1]) if len(sys.argv) > 1 else (1 << 30)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    fine = "--fine" in sys.argv
+    max_bytes = int(args[0]) if args else (1 << 30)
     vc.init(0)
     _, eff = bench.effective_cpus()
     rows = []
     rng = np.random.default_rng(5)
     for mtu in (1024, 16404, 65536):
         flen = mtu - 4
-        for W in (16, 64, 256, 1024, 4096, 16384, 65535):
+        ws = ([max(1, (m << 20) // flen) for m in range(16, 73, 8)] if fine
+              else (16, 64, 256, 1024, 4096, 16384, 65535))
+        for W in ws:
             if W * mtu > max_bytes:
                 continue
             stream = rng.integers(0, 256, W * mtu, dtype=np.uint8)

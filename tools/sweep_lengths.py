@@ -9,7 +9,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import val_protocol_amd.crc as vc  # noqa: E402
-from tools.sweep_geometry import time_it  # noqa: E402
+from tools.ab_libs import time_it  # noqa: E402
 
 
 def main():

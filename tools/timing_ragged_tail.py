@@ -38,6 +38,7 @@ order = np.argsort(end)
 pct = lambda a: " ".join(f"{np.percentile(a, q):7.1f}" for q in (0, 10, 50, 90, 100))
 print(f"{name}: waves={used.sum()} end {pct(end)}")
 print("  last-item duration", pct(end - last))
+print("  prologue (LDS fill) end", pct(us[:, 1]))
 for c in range(4):
     m = cls == c
     if m.any():

@@ -72,8 +72,27 @@ def build(verbose: bool = True, out: str = OUT, build_dir: str = BUILD) -> str:
           os.path.join(CSRC, "cpu_crc32.c"), "-o", cpu_o], verbose)
     _run(["gcc", "-O2", "-fPIC", "-std=c99", "-Wall", "-Wextra", "-Werror", f"-I{INC}", "-c",
           os.path.join(CSRC, "val_batch.c"), "-o", batch_o], verbose)
-    _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror", f"-I{INC}", f"-I{CSRC}",
-          "-c", os.path.join(CSRC, "val_crc32_hip.hip"), "-o", hip_o], verbose)
+    hip_cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Werror", f"-I{INC}",
+               f"-I{CSRC}", "-c", os.path.join(CSRC, "val_crc32_hip.hip"), "-o", hip_o]
+    # The HIP object takes minutes: it is rebuilt only when a file it includes
+    # (every header and the .hip itself) or its command changed.
+    hip_stamp = hip_o + ".srchash"
+    h = hashlib.sha256(" ".join(hip_cmd).encode())
+    for f in sources():
+        if not f.endswith(".c") and not f.endswith(".py"):
+            h.update(os.path.relpath(f, ROOT).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    hip_digest = h.hexdigest()
+    try:
+        with open(hip_stamp) as fh:
+            hip_current = os.path.exists(hip_o) and fh.read().strip() == hip_digest
+    except OSError:
+        hip_current = False
+    if not hip_current:
+        _run(hip_cmd, verbose)
+        with open(hip_stamp, "w") as fh:
+            fh.write(hip_digest + "\n")
     fd, tmp = tempfile.mkstemp(prefix=".libval_crc_hip.", suffix=".so", dir=os.path.dirname(out))
     os.close(fd)
     try:

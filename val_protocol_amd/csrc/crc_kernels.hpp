@@ -960,7 +960,9 @@ __global__ __launch_bounds__(kBlock) void k_frames_ragged(const FrameParams p)
     // The first item's frame loads wait on three dependent reads (plan, sorted
     // order, descriptors), so the LDS fill is not overlapped with them here:
     // its registers would be live through the loop (a spill at 128 VGPRs).
+#ifndef VCRC_NO_LDS_FILL  // diagnostic A/B builds only (wrong CRCs): the upper bound of overlapping the fill
     build_lds_tables(p.consts);
+#endif
     if (PAY) lds_pow_maps(p.consts);
     __syncthreads();
     VCRC_STAMP(1);

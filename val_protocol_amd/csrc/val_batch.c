@@ -68,10 +68,12 @@ struct val_batch {
 };
 
 static val_batch_t *volatile g_reg[VB_MAX_ATTACHED];
+static int g_hwm;  /* slots [0, g_hwm) have been used: the provider scans only those */
 
 static val_batch_t *vb_lookup(const void *buf, int rx)
 {
-    for (int i = 0; i < VB_MAX_ATTACHED; i++) {
+    const int hwm = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
+    for (int i = 0; i < hwm; i++) {
         val_batch_t *b = __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
         if (b && (rx ? (const void *)b->recv_buffer : (const void *)b->send_buffer) == buf) return b;
     }
@@ -430,6 +432,11 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     for (int i = 0; i < VB_MAX_ATTACHED && slot < 0; i++) {
         val_batch_t *expect = NULL;
         if (__atomic_compare_exchange_n(&g_reg[i], &expect, b, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) slot = i;
+    }
+    if (slot >= 0) {
+        int h = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
+        while (h < slot + 1 && !__atomic_compare_exchange_n(&g_hwm, &h, slot + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+        }
     }
     if (!b->tx || !b->rx || !b->txf || !b->rxf || !b->crc_tmp || !b->off_tmp || !b->len_tmp || slot < 0) {
         if (slot >= 0) __atomic_store_n(&g_reg[slot], NULL, __ATOMIC_RELEASE);

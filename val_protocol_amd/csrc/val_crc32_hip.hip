@@ -1180,19 +1180,30 @@ val_status_t frames_host_small(Ctx &c, const uint8_t *base, uint64_t lo, uint64_
 // and count, payload states. Counted (val_gpu_cpu_batch_count);
 // VAL_GPU_HOST_BATCH_MIN_BYTES or val_gpu_set_host_batch_min_bytes moves the
 // threshold (0 = always the GPU: the GPU test suite sets it).
-#ifndef VCRC_HOST_BATCH_MIN_BYTES  // measured crossover at one CPU thread, DESIGN.md section 1
+// The crossover depends on the frame size: the CPU engine folds long frames
+// from DRAM about twice as fast as 1 KiB frames, so at one CPU thread the GPU
+// path (pageable) wins from about 32 MiB of 1 KiB frames but only past 64 MiB
+// of 16-64 KiB frames (profiles/r04_host_crossover.jsonl, r05_host_crossover_
+// fine.jsonl). The default is therefore chosen by the batch's mean CRC input
+// per frame; a value set by the environment or the setter applies to all.
+#ifndef VCRC_HOST_BATCH_MIN_BYTES  // measured crossover at one CPU thread, frames of >= 4 KiB
 #define VCRC_HOST_BATCH_MIN_BYTES (64u << 20)
 #endif
+#ifndef VCRC_HOST_BATCH_MIN_BYTES_SHORT  // the same for a mean frame under 4 KiB
+#define VCRC_HOST_BATCH_MIN_BYTES_SHORT (32u << 20)
+#endif
+constexpr uint64_t kShortFrameMean = 4096;
 std::atomic<int64_t> g_host_batch_min{-1};  // -1: from the environment, else the default
 std::atomic<uint32_t> g_host_cpu_threads{1};
 std::atomic<uint64_t> g_cpu_batches{0};
 
-uint64_t host_batch_min_bytes()
+uint64_t host_batch_min_bytes(uint64_t mean_len = UINT64_MAX)
 {
     const int64_t v = g_host_batch_min.load(std::memory_order_relaxed);
     if (v >= 0) return (uint64_t)v;
     static const int64_t env = env_size("VAL_GPU_HOST_BATCH_MIN_BYTES");
-    return env >= 0 ? (uint64_t)env : (uint64_t)VCRC_HOST_BATCH_MIN_BYTES;
+    if (env >= 0) return (uint64_t)env;
+    return mean_len < kShortFrameMean ? (uint64_t)VCRC_HOST_BATCH_MIN_BYTES_SHORT : (uint64_t)VCRC_HOST_BATCH_MIN_BYTES;
 }
 
 std::vector<uint32_t> shard_cuts(uint32_t n, const uint32_t *len, uint32_t world);
@@ -1291,7 +1302,7 @@ val_status_t frames_host(const uint8_t *base, uint64_t base_len, const uint64_t 
         total += l;
         if (off && i && off[i] < off[i - 1]) monotone = false;
     }
-    if (route_cpu && total < host_batch_min_bytes()) {  // below the crossover: the CPU engine (no device needed)
+    if (route_cpu && total < host_batch_min_bytes(n ? total / n : 0)) {  // below the crossover: the CPU engine
         const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, pay);
         if (nbad) *nbad = verify ? bad : 0u;
         return VAL_OK;
@@ -1471,10 +1482,10 @@ void shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t rank
 // scales with its T threads (val_gpu_set_host_cpu_threads, capped by the
 // CPU budget). First-order crossover: C(N, T) = C1 * T / N (DESIGN.md
 // section 1). A GPU test that forces C1 = 0 keeps every batch on the GPU.
-uint64_t host_multi_min_bytes(int devices)
+uint64_t host_multi_min_bytes(int devices, uint64_t mean_len = UINT64_MAX)
 {
     const uint64_t t = std::max<uint64_t>(1, std::min<uint64_t>(g_host_cpu_threads.load(), host_cpu_budget()));
-    return host_batch_min_bytes() * t / (uint64_t)std::max(1, devices);
+    return host_batch_min_bytes(mean_len) * t / (uint64_t)std::max(1, devices);
 }
 
 // Run work(0..k-1): k-1 helper threads plus the calling thread; a helper that
@@ -1518,7 +1529,7 @@ val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uin
     if (ndev <= 0) ndev = std::max(1, std::min(count, kMaxDevices));
     ndev = std::min(ndev, kMaxDevices);
     // one decision for the whole batch: distinct devices the shards land on
-    if (total < host_multi_min_bytes(std::max(1, std::min(ndev, count)))) {
+    if (total < host_multi_min_bytes(std::max(1, std::min(ndev, count)), n ? total / n : 0)) {
         const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, nullptr);
         if (nbad) *nbad = verify ? bad : 0u;
         return VAL_OK;
