@@ -46,6 +46,9 @@
  *       the same transfer with the product's window batcher attached to both
  *       configs (include/val_batch.h: TX trailers from one frames_host call
  *       per window fill, RX frames read ahead and checked from one call).
+ *   provider_harness <libval_crc_hip.so> loopback-batched-par <bytes> <mtu> <window> <pairs>
+ *       `pairs` batched transfers at once (two threads each): the batcher's
+ *       registry and the library under concurrent sessions.
  *   provider_harness <libval_crc_hip.so> sessions | sessions-batched
  *       the five recorded sessions of `none sessions` (windowed, resumed)
  *       re-run with the product's provider installed, plain or batched;
@@ -373,7 +376,7 @@ static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
     return 0;
 }
 
-static void batch_report(void *ba, void *bb)
+static void batch_report(FILE *out, void *ba, void *bb)
 {
     fn_bstats_t gs = (fn_bstats_t)dlsym(g_lib, "val_batch_get_stats");
     fn_bdetach_t dt = (fn_bdetach_t)dlsym(g_lib, "val_batch_detach");
@@ -381,9 +384,9 @@ static void batch_report(void *ba, void *bb)
     memset(st, 0, sizeof st);
     gs(ba, &st[0]);
     gs(bb, &st[1]);
-    printf(",\"batch\":[");
+    fprintf(out, ",\"batch\":[");
     for (int k = 0; k < 2; k++)
-        printf("%s{\"end\":\"%s\",\"tx_frames\":%llu,\"tx_batched_frames\":%llu,\"tx_batches\":%llu,\"tx_max_batch\":%llu,"
+        fprintf(out, "%s{\"end\":\"%s\",\"tx_frames\":%llu,\"tx_batched_frames\":%llu,\"tx_batches\":%llu,\"tx_max_batch\":%llu,"
                "\"rx_frames\":%llu,\"rx_batches\":%llu,\"rx_max_batch\":%llu,\"rx_batched_answers\":%llu,"
                "\"direct_answers\":%llu,\"status\":%d}",
                k ? "," : "", k ? "receiver" : "sender", (unsigned long long)st[k].tx_frames,
@@ -391,7 +394,7 @@ static void batch_report(void *ba, void *bb)
                (unsigned long long)st[k].tx_max_batch, (unsigned long long)st[k].rx_frames,
                (unsigned long long)st[k].rx_batches, (unsigned long long)st[k].rx_max_batch,
                (unsigned long long)st[k].rx_batched_answers, (unsigned long long)st[k].direct_answers, st[k].status);
-    printf("]");
+    fprintf(out, "]");
     dt(ba);
     dt(bb);
 }
@@ -670,7 +673,8 @@ static unsigned long trailers_ok(const end_t *e)
     return n;
 }
 
-static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window, int batched)
+static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, uint16_t window, int batched,
+                        uint64_t seed)
 {
     char tmpl[] = "/tmp/valgpuXXXXXX";
     char *dir = mkdtemp(tmpl);
@@ -681,7 +685,7 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window,
     snprintf(out, sizeof out, "%s/out/input.bin", dir);
     mkdir(outdir, 0777);
     uint8_t *data = (uint8_t *)malloc(bytes ? bytes : 1);
-    oracle_prng_fill(0x10AD, data, bytes);
+    oracle_prng_fill(seed, data, bytes);
     FILE *f = fopen(in, "wb");
     fwrite(data, 1, bytes, f);
     fclose(f);
@@ -730,7 +734,7 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window,
         equal = (r == bytes) && memcmp(back, data, bytes) == 0;
         free(back);
     }
-    printf("{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
+    fprintf(out_json, "{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
            "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
            "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"flipped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
@@ -743,17 +747,75 @@ static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window,
            (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
     val_session_destroy(tx);
     val_session_destroy(rx);
-    if (batched) batch_report(ba, bb);
-    printf("}\n");
+    if (batched) batch_report(out_json, ba, bb);
+    fprintf(out_json, "}\n");
     for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
     for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
     free(etx.log);
     free(erx.log);
+    free(data);
     remove(out);
     remove(in);
     rmdir(outdir);
     rmdir(dir);
     return 0;
+}
+
+static int mode_loopback(size_t bytes, size_t mtu, int use_gpu, uint16_t window, int batched)
+{
+    return loopback_run(stdout, bytes, mtu, use_gpu, window, batched, 0x10AD);
+}
+
+/* `pairs` batched loopback transfers at once, one sender and one receiver
+ * thread each: every session's provider calls and window batches go through
+ * the one process-wide batcher registry and the product library at the same
+ * time (reference include/val_protocol.h:231-233: sessions run in parallel). */
+typedef struct {
+    size_t bytes, mtu;
+    uint16_t window;
+    uint64_t seed;
+    char *buf;
+    size_t len;
+    int rc;
+} par_job_t;
+
+static void *par_main(void *arg)
+{
+    par_job_t *j = (par_job_t *)arg;
+    FILE *m = open_memstream(&j->buf, &j->len);
+    j->rc = loopback_run(m, j->bytes, j->mtu, 1, j->window, 1, j->seed);
+    fclose(m);
+    return NULL;
+}
+
+static int mode_loopback_par(size_t bytes, size_t mtu, uint16_t window, int pairs)
+{
+    par_job_t *jobs = (par_job_t *)calloc((size_t)pairs, sizeof(par_job_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)pairs, sizeof(pthread_t));
+    const uint64_t cpu_b0 = lib_count("val_gpu_cpu_batch_count"), cpu_s0 = lib_count("val_gpu_cpu_small_count"),
+                   cpu_f0 = lib_count("val_gpu_cpu_fallback_count");
+    for (int i = 0; i < pairs; i++) {
+        jobs[i] = (par_job_t){bytes, mtu, window, 0x10AD + 977u * (uint64_t)i, NULL, 0, 0};
+        pthread_create(&th[i], NULL, par_main, &jobs[i]);
+    }
+    int rc = 0;
+    printf("{\"mode\":\"loopback-batched-par\",\"pairs\":%d,\"lib_cpu_batches\":", pairs);
+    for (int i = 0; i < pairs; i++) pthread_join(th[i], NULL);
+    printf("%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu,\"runs\":[",
+           (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
+           (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
+           (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
+    for (int i = 0; i < pairs; i++) {
+        size_t n = jobs[i].len;
+        while (n && (jobs[i].buf[n - 1] == '\n')) n--;
+        printf("%s%.*s", i ? "," : "", (int)n, jobs[i].buf);
+        rc |= jobs[i].rc;
+        free(jobs[i].buf);
+    }
+    printf("]}\n");
+    free(jobs);
+    free(th);
+    return rc;
 }
 
 /* ---- fixtures: drop-in golden vectors, reference built-in CRC only --------
@@ -1197,7 +1259,7 @@ static int fx_session(const char *name, size_t bytes, size_t mtu, uint16_t windo
     }
     val_session_destroy(tx);
     val_session_destroy(rx);
-    if (batched) batch_report(ba, bb);
+    if (batched) batch_report(stdout, ba, bb);
     printf("}%s\n", last ? "" : ",");
     for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
     for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
@@ -1276,6 +1338,10 @@ int main(int argc, char **argv)
     if (!strcmp(argv[2], "loopback-batched") && argc >= 6)
         return use_gpu ? mode_loopback((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), 1,
                                        (uint16_t)strtoul(argv[5], NULL, 0), 1)
+                       : 1;
+    if (!strcmp(argv[2], "loopback-batched-par") && argc >= 7)
+        return use_gpu ? mode_loopback_par((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0),
+                                           (uint16_t)strtoul(argv[5], NULL, 0), atoi(argv[6]))
                        : 1;
     if (!strcmp(argv[2], "sessions")) return use_gpu ? mode_sessions(counting_provider, 0) : 1;
     if (!strcmp(argv[2], "sessions-batched")) return use_gpu ? mode_sessions(counting_provider, 1) : 1;

@@ -184,3 +184,25 @@ def test_corrupted_frames_detected_like_the_reference(gpu):
     finally:
         for k in env:
             os.environ.pop(k, None)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
+def test_parallel_batched_sessions(gpu):
+    """Four batched transfers at once (eight session threads; reference
+    include/val_protocol.h:231-233: sessions run in parallel): every
+    session's provider calls resolve to its own batcher through the shared
+    registry, and every window of every session goes through the library
+    concurrently; each transfer ends clean with every trailer equal to the
+    reference's own CRC."""
+    out = json.loads(_run([vc.LIB_PATH, "loopback-batched-par", 2_000_000, 4096, 32, 4], gpu))
+    assert len(out["runs"]) == 4
+    if gpu:
+        assert out["lib_cpu_batches"] == 0 and out["lib_cpu_small"] == 0
+    assert out["lib_cpu_fallbacks"] == 0
+    for r in out["runs"]:
+        assert r["tx_status"] == VAL_OK and r["rx_status"] == VAL_OK and r["equal"] == 1, r
+        assert r["rx_crc_errors"] == 0 and r["trailers_ok"] == r["tx_frames"] + r["rx_frames"]
+        tx, rx = r["batch"]
+        assert tx["tx_max_batch"] == 32 and tx["status"] == VAL_OK and rx["status"] == VAL_OK
+        assert rx["rx_batched_answers"] >= 2_000_000 // (4096 - 12)
