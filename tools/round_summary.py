@@ -42,6 +42,10 @@ def traffic(o, fetch, write, cfg, out_name):
          "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
          "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wr) / alg,
          "correction": "gfx950: FETCH_SIZE x1024 x2 (half-count of 16 B/lane streaming reads), WRITE_SIZE x1024"}
+    prov = os.path.join(o, "provenance.json")
+    if os.path.exists(prov):  # bench.py reports it as roofline.traffic_source
+        d["source"] = dict(json.load(open(prov)), method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate "
+                                                          "passes over tools/prof_target.py (3 launches)")
     with open(os.path.join(ROOT, "profiles", out_name), "w") as f:
         json.dump(d, f, indent=1)
     return d
@@ -93,9 +97,9 @@ def main():
         q = s["pmc_sq_cfg3_per_launch"]
         s["sq_wait_any_over_wave_cycles"] = q["SQ_WAIT_ANY"] / q["SQ_WAVE_CYCLES"]
         s["lds_bank_conflict_cycles_per_lds_instr"] = q["SQ_LDS_BANK_CONFLICT"] / q["SQ_INSTS_LDS"]
-    hi = os.path.join(o, "host_inclusive.log")
-    if os.path.exists(hi):
-        s["host_inclusive_log"] = open(hi).read().strip().splitlines()[-3:]
+    prov = os.path.join(o, "provenance.json")
+    if os.path.exists(prov):
+        s["provenance"] = json.load(open(prov))
     pt = os.path.join(o, "pytest_gpu.log")
     if os.path.exists(pt):
         s["pytest_gpu_tail"] = open(pt).read().strip().splitlines()[-2:]
