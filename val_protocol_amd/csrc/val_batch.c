@@ -38,7 +38,8 @@ struct val_batch {
     val_batch_opts_t opt;
     const uint8_t *send_buffer, *recv_buffer;
     size_t mtu;
-    int pinned;
+    int pinned;              /* allocate windows pinned (a device is present) */
+    int tx_pinned, rx_pinned; /* how each window buffer was allocated */
     /* TX window */
     uint8_t *tx;
     size_t tx_used;
@@ -377,20 +378,17 @@ uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
 }
 
 /* ---- lifetime ---------------------------------------------------------- */
-static void *vb_alloc(val_batch_t *b, size_t n)
+static void *vb_alloc(const val_batch_t *b, size_t n, int *pinned)
 {
     void *p = b->pinned ? val_gpu_host_alloc(n) : NULL;
-    if (!p) {
-        b->pinned = 0;
-        p = malloc(n);
-    }
-    return p;
+    *pinned = p != NULL;
+    return p ? p : malloc(n);
 }
 
-static void vb_free(val_batch_t *b, void *p)
+static void vb_free(void *p, int pinned)
 {
     if (!p) return;
-    if (b->pinned) val_gpu_host_free(p);
+    if (pinned) val_gpu_host_free(p);
     else free(p);
 }
 
@@ -421,8 +419,8 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     b->recv_buffer = (const uint8_t *)cfg->buffers.recv_buffer;
     b->pinned = val_gpu_device_count() > 0;  /* pinned windows: DMA in place on the GPU path */
     const uint32_t nf = b->opt.max_frames;
-    b->tx = (uint8_t *)vb_alloc(b, b->opt.max_bytes);
-    b->rx = (uint8_t *)vb_alloc(b, b->opt.max_bytes);
+    b->tx = (uint8_t *)vb_alloc(b, b->opt.max_bytes, &b->tx_pinned);
+    b->rx = (uint8_t *)vb_alloc(b, b->opt.max_bytes, &b->rx_pinned);
     b->txf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
     b->rxf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
     b->crc_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
@@ -440,8 +438,8 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     }
     if (!b->tx || !b->rx || !b->txf || !b->rxf || !b->crc_tmp || !b->off_tmp || !b->len_tmp || slot < 0) {
         if (slot >= 0) __atomic_store_n(&g_reg[slot], NULL, __ATOMIC_RELEASE);
-        vb_free(b, b->tx);
-        vb_free(b, b->rx);
+        vb_free(b->tx, b->tx_pinned);
+        vb_free(b->rx, b->rx_pinned);
         free(b->txf);
         free(b->rxf);
         free(b->crc_tmp);
@@ -491,8 +489,8 @@ void val_batch_detach(val_batch_t *b)
     cfg->transport.flush = b->u_flush;
     cfg->transport.io_context = b->u_io;
     cfg->crc32_provider = b->u_provider;
-    vb_free(b, b->tx);
-    vb_free(b, b->rx);
+    vb_free(b->tx, b->tx_pinned);
+    vb_free(b->rx, b->rx_pinned);
     free(b->txf);
     free(b->rxf);
     free(b->crc_tmp);
