@@ -69,8 +69,12 @@ def kernel_trace(o, sub, rnd, tag, prefer=None):
     top = max(pick, key=lambda r: float(r["TotalDurationNs"]))
     main = [r for r in crc if r["Kernel_Name"] == top["Name"]]
     steps = int(os.environ.get("BENCH_STEPS", "20"))  # bench.py's timed steps (default 20, after 15 warmup)
-    extra = min(steps, 5)  # bench.py's untimed per-step pass after the timed region (round 3 on)
-    timed = main[-(steps + extra):-extra] if len(main) >= steps + extra else main[-steps:]
+    warmup = int(os.environ.get("BENCH_WARMUP", "15"))
+    # bench.py launches nothing of this kernel before its warmup steps (non-verify
+    # runs); after the timed steps come its per-step pass, the host_inclusive
+    # block and (cfg5) the verify windows, so the timed launches are counted
+    # from the front
+    timed = main[warmup:warmup + steps]
     last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     return {"kernel": top["Name"], "dispatches": int(top["Calls"]), "avg_ms_all_dispatches": float(top["AverageNs"]) / 1e6,
             "timed_dispatches": len(last),
