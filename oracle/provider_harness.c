@@ -116,7 +116,9 @@ static int pipe_push(pipe_t *p, const uint8_t *d, size_t n)
         pthread_mutex_unlock(&p->mu);
         return -1;
     }
-    for (size_t i = 0; i < n; i++) p->buf[(p->head + p->len + i) % p->cap] = d[i];
+    const size_t at = (p->head + p->len) % p->cap, first = n < p->cap - at ? n : p->cap - at;
+    memcpy(p->buf + at, d, first);  /* the ring's two pieces */
+    memcpy(p->buf, d + first, n - first);
     p->len += n;
     pthread_cond_broadcast(&p->cv);
     pthread_mutex_unlock(&p->mu);
@@ -137,7 +139,9 @@ static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
             return 0;
         }
     }
-    for (size_t i = 0; i < n; i++) d[i] = p->buf[(p->head + i) % p->cap];
+    const size_t first = n < p->cap - p->head ? n : p->cap - p->head;
+    memcpy(d, p->buf + p->head, first);
+    memcpy(d + first, p->buf, n - first);
     p->head = (p->head + n) % p->cap;
     p->len -= n;
     pthread_mutex_unlock(&p->mu);
