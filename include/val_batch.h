@@ -76,10 +76,11 @@ typedef struct {
 typedef struct val_batch val_batch_t;
 
 /* Wrap cfg->transport and cfg->crc32_provider (cfg->buffers.send_buffer,
- * recv_buffer and packet_size must be set). opts may be NULL (defaults: TX
- * and RX batching on). cfg must outlive the session; call
- * val_batch_detach after val_session_destroy. Up to 256 attached configs
- * per process. */
+ * recv_buffer and packet_size must be set; the two buffers must differ and
+ * not belong to another attached config: VAL_ERR_INVALID_ARG otherwise).
+ * opts may be NULL (defaults: TX and RX batching on). Attach before
+ * val_session_create (the session copies the config); call val_batch_detach
+ * after val_session_destroy. Up to 256 attached configs per process. */
 val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out);
 /* Send the staged TX window now (the wrapped hooks do this themselves). */
 val_status_t val_batch_flush(val_batch_t *b);

@@ -75,3 +75,53 @@ def test_no_gpu_means_loud_failure_not_fallback():
     with pytest.raises(vc.ValError) as e:
         vc.init(0)
     assert e.value.status == vc.VAL_ERR_IO
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_batch_attach_argument_checks():
+    """val_batch_attach (include/val_batch.h) refuses configs the provider
+    could not tell apart: one buffer for both directions, or a buffer that
+    another attached config already uses; detach restores the hooks. No
+    GPU needed (the window buffers are plain host memory then)."""
+    src = r"""
+    #include "val_batch.h"
+    #include <stdio.h>
+    #include <string.h>
+    static int snd(void *c, const void *d, size_t n) { (void)c; (void)d; return (int)n; }
+    static int rcv(void *c, void *b, size_t n, size_t *g, unsigned t) { (void)c; (void)b; (void)n; (void)t; *g = 0; return 0; }
+    static char a[2048], b[2048], c[2048];
+    int main(void) {
+        val_config_t x, y;
+        memset(&x, 0, sizeof x);
+        x.transport.send = snd;
+        x.transport.recv = (int (*)(void *, void *, size_t, size_t *, uint32_t))rcv;
+        x.buffers.packet_size = 2048;
+        x.buffers.send_buffer = a;
+        x.buffers.recv_buffer = a;
+        val_batch_t *bx = NULL, *by = NULL;
+        int r1 = val_batch_attach(&x, NULL, &bx);          /* same buffer both ways */
+        x.buffers.recv_buffer = b;
+        int r2 = val_batch_attach(&x, NULL, &bx);          /* fine */
+        int hooked = x.transport.send != snd && x.crc32_provider == val_batch_crc32_provider;
+        y = x;
+        y.transport.send = snd;
+        y.buffers.send_buffer = c;                          /* recv_buffer b is taken */
+        int r3 = val_batch_attach(&y, NULL, &by);
+        val_batch_detach(bx);
+        int restored = x.transport.send == snd && x.crc32_provider == NULL;
+        int r4 = val_batch_attach(&y, NULL, &by);          /* b is free again */
+        val_batch_detach(by);
+        printf("%d %d %d %d %d %d\n", r1, r2, hooked, r3, restored, r4);
+        return 0;
+    }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        libdir = os.path.dirname(vc.LIB_PATH)
+        vc.lib()  # built and current
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{INC}", c, "-o", exe, f"-L{libdir}",
+                        "-l:libval_crc_hip.so", f"-Wl,-rpath,{libdir}"], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    assert [int(v) for v in out] == [vc.VAL_ERR_INVALID_ARG, 0, 1, vc.VAL_ERR_INVALID_ARG, 1, 0]

@@ -252,7 +252,10 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
                 break;
             }
             b->owe = content + VAL_WIRE_TRAILER_SIZE;
-            const long r = vb_read(b, b->rx + b->r_len, b->owe, timeout_ms);
+            /* the asked-for frame waits as the session would; a frame read
+               ahead takes only what is there already, so the frames before it
+               are not held back by a late body */
+            const long r = vb_read(b, b->rx + b->r_len, b->owe, first ? timeout_ms : 0u);
             if (r < 0) return -1;
             b->r_len += (size_t)r;
             b->owe -= (size_t)r;
@@ -335,6 +338,7 @@ static int vb_recv(void *ctx, void *buffer, size_t size, size_t *received, uint3
 {
     val_batch_t *b = (val_batch_t *)ctx;
     if (received) *received = 0;
+    if (size == 0) return 0;
     /* the session is about to wait: its staged window goes out first */
     if (vb_flush_tx(b) != VAL_OK) return -1;
     if (!b->opt.rx) return b->u_recv(b->u_io, buffer, size, received, timeout_ms);
@@ -397,6 +401,13 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     if (!cfg || !out || !cfg->transport.send || !cfg->transport.recv || !cfg->buffers.send_buffer ||
         !cfg->buffers.recv_buffer || cfg->buffers.packet_size < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE)
         return VAL_ERR_INVALID_ARG;
+    /* the provider tells TX from RX by the buffer: they must be distinct, and
+       not already attached for another session */
+    if (cfg->buffers.send_buffer == cfg->buffers.recv_buffer)
+        return VAL_ERR_INVALID_ARG;
+    for (int role = 0; role < 2; role++)
+        if (vb_lookup(cfg->buffers.send_buffer, role) || vb_lookup(cfg->buffers.recv_buffer, role))
+            return VAL_ERR_INVALID_ARG;
     val_batch_t *b = (val_batch_t *)calloc(1, sizeof *b);
     if (!b) return VAL_ERR_NO_MEMORY;
     if (opts) b->opt = *opts;
