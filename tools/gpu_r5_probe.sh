@@ -1,7 +1,8 @@
-# Round-5 probe: ragged class lanes (VCRC_CLASS_LANES variants V1..V3) against
-# the product (A), back to back, on the cfg5 mix, the class-2 mix and
-# uniform short frames through the ragged path.
+# Round-5 probe: k_region_dyn parity (region tests) and its same-box A/B
+# against the one-chunk-per-wave k_region (build/libval_A.so).
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/g4; mkdir -p $O
-timeout -k 10 400 python tools/ab_b2b.py build/libval_A.so build/libval_V1.so build/libval_V2.so build/libval_V3.so cfg5log c2 u1100 u3000 > $O/ab_lanes.log 2>&1
-rc=$?; echo "rc=$rc"; grep -v amdgpu $O/ab_lanes.log; exit $rc
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/g7; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k region -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python tools/ab_region.py build/libval_A.so build/libval_B.so 8388608 33554432 67108864 134217728 268435456 1073741824 > $O/ab_region.log 2>&1
+rc=$?; grep -v amdgpu $O/ab_region.log; exit $rc

@@ -18,8 +18,9 @@ vc._lib.vcrc_debug_times.argtypes = [ctypes.c_void_p]
 vc._lib.vcrc_debug_times.restype = ctypes.c_int
 vc.init(0)
 dev = torch.device("cuda:0")
-big = torch.randint(0, 256, (64 << 20,), dtype=torch.uint8, device=dev)
-for size in [int(x) for x in sys.argv[2:]]:
+sizes = [int(x) for x in sys.argv[2:]]
+big = torch.randint(0, 256, (max(sizes),), dtype=torch.uint8, device=dev)
+for size in sizes:
     buf = np.zeros(4096 * 4, np.uint64)
     for rep in range(3):
         vc._lib.vcrc_debug_times(buf.ctypes.data)  # (reset not needed: stamps overwrite)
@@ -39,3 +40,5 @@ for size in [int(x) for x in sys.argv[2:]]:
     print(f"region {size} B: waves stamped {nw}")
     for k, name in enumerate(("start", "issued", "barrier", "hashed")):
         print(f"  {name:9s}", pct(us[used, k]))
+    hashed = us[used, 3]
+    print("  hashed percentiles 10/25/75/90:", " ".join(f"{np.percentile(hashed, q):6.2f}" for q in (10, 25, 75, 90)))
