@@ -1,8 +1,6 @@
-# Round-5 probe: k_region_dyn parity (region tests) and its same-box A/B
-# against the one-chunk-per-wave k_region (build/libval_A.so).
+# Round-5 probe: the driver's default 8-GPU bench invocation (cfg3 + cfg4_strong
+# + host_inclusive on rank 0) rehearsed as 8 gloo ranks on one GPU.
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/g7; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k region -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
-rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python tools/ab_region.py build/libval_A.so build/libval_B.so 8388608 33554432 67108864 134217728 268435456 1073741824 > $O/ab_region.log 2>&1
-rc=$?; grep -v amdgpu $O/ab_region.log; exit $rc
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/g8; mkdir -p $O
+VAL_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 8 --steps 3 --warmup 1 > $O/bench8.json 2> $O/bench8.err
+rc=$?; echo "rc=$rc"; tail -c 3000 $O/bench8.json; tail -5 $O/bench8.err; exit $rc
