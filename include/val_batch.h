@@ -23,8 +23,12 @@
  *       reference's, byte for byte; only the time of sending moves to the
  *       end of the window fill.
  *   RX: the wrapped transport.recv reads ahead: the frame the session asked
- *       for plus every further frame the transport already holds (polled
- *       with a zero timeout), up to the window limits, and computes their
+ *       for (over as many short reads as the transport returns, within the
+ *       session's timeout, measured with config->system.get_ticks_ms) plus
+ *       every further frame the transport already holds (polled with a zero
+ *       timeout while polls return bytes), up to the window limits; no byte
+ *       read is ever dropped (a frame cut off by a poll finishes in the next
+ *       read-ahead and is delivered unbatched). It computes their
  *       CRCs with ONE val_crc32_frames_host call. It hands bytes to the
  *       session exactly as asked; when a frame's header and content were
  *       delivered to recv_buffer in place and its trailer after them, the

@@ -125,6 +125,38 @@ static int pipe_push(pipe_t *p, const uint8_t *d, size_t n)
     return (int)n;
 }
 
+/* Pop exactly n bytes within timeout_ms (0 = nothing, 1 = popped); with
+ * upto != 0, pop as soon as any byte is there, at most min(n, upto) of them,
+ * and return the count (a transport that delivers partial reads, as the
+ * reference's net simulator can: unit_tests/support/test_support.c:655-816). */
+static size_t pipe_pop_upto(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms, size_t upto)
+{
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += timeout_ms / 1000u;
+    dl.tv_nsec += (long)(timeout_ms % 1000u) * 1000000L;
+    if (dl.tv_nsec >= 1000000000L) { dl.tv_sec++; dl.tv_nsec -= 1000000000L; }
+    pthread_mutex_lock(&p->mu);
+    const size_t need = upto ? 1 : n;
+    while (p->len < need) {
+        if (pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
+            pthread_mutex_unlock(&p->mu);
+            return 0;
+        }
+    }
+    if (upto) {
+        n = n < upto ? n : upto;
+        n = n < p->len ? n : p->len;
+    }
+    const size_t first = n < p->cap - p->head ? n : p->cap - p->head;
+    memcpy(d, p->buf + p->head, first);
+    memcpy(d + first, p->buf, n - first);
+    p->head = (p->head + n) % p->cap;
+    p->len -= n;
+    pthread_mutex_unlock(&p->mu);
+    return upto ? n : 1;
+}
+
 static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
 {
     struct timespec dl;
@@ -203,10 +235,28 @@ static int tp_send(void *ctx, const void *data, size_t len)
     return pipe_push(e->out, (const uint8_t *)data, len);
 }
 
+/* VAL_HARNESS_PARTIAL=N: every transport.recv returns at most N bytes (and
+ * whatever is there, once anything is): partial reads, which val_recv_full
+ * (src/val_core.c:12-43) loops over. */
+static size_t partial_env(void)
+{
+    static long v = -1;
+    if (v < 0) {
+        const char *e = getenv("VAL_HARNESS_PARTIAL");
+        v = e ? (long)strtoul(e, NULL, 0) : 0;
+    }
+    return (size_t)v;
+}
+
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
 {
     end_t *e = (end_t *)ctx;
     e->recvs++;
+    if (partial_env()) {
+        const size_t n = pipe_pop_upto(e->in, (uint8_t *)buffer, size, timeout_ms, partial_env());
+        if (got) *got = n;
+        return 0;
+    }
     if (pipe_pop(e->in, (uint8_t *)buffer, size, timeout_ms)) {
         if (got) *got = size;
     } else if (got) {

@@ -206,3 +206,41 @@ def test_parallel_batched_sessions(gpu):
         tx, rx = r["batch"]
         assert tx["tx_max_batch"] == 32 and tx["status"] == VAL_OK and rx["status"] == VAL_OK
         assert rx["rx_batched_answers"] >= 2_000_000 // (4096 - 12)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
+def test_partial_read_transport(gpu):
+    """A transport whose recv returns at most 7 bytes a call (the reference
+    tolerates short reads: src/val_core.c:12-43, and its net simulator makes
+    them: unit_tests/support/test_support.c:655-816). At window 1 the wire is
+    the whole-read run's byte for byte, with the plain provider and with the
+    batcher, and the batcher still reads frames ahead and answers every
+    receiver check from a batch (its read-ahead completes a frame over as many
+    short reads as the session's timeout allows). At window 32 the batched
+    transfer ends clean with full-window read-ahead batches; the reference's
+    own outcome there depends on timing (a timeout in mid-frame drops the
+    bytes val_recv_full had, src/val_core.c:39-40), so it is not compared."""
+    whole = _line(_run(["none", "loopback", 1 << 20, 1024], gpu))
+    os.environ["VAL_HARNESS_PARTIAL"] = "7"
+    try:
+        for mode in (["none", "loopback", 1 << 20, 1024], [vc.LIB_PATH, "loopback", 1 << 20, 1024],
+                     [vc.LIB_PATH, "loopback-batched", 1 << 20, 1024, 0]):
+            got = _line(_run(mode, gpu))
+            for k in ("tx_status", "rx_status", "equal", "tx_digest", "rx_digest", "tx_frames", "rx_frames",
+                      "retransmits"):
+                assert got[k] == whole[k], (mode[1], k, got[k], whole[k])
+            if mode[0] != "none":
+                _lib_counters_clean(got, gpu)
+            if mode[1] == "loopback-batched":
+                rx = got["batch"][1]
+                assert rx["status"] == VAL_OK and rx["direct_answers"] == 0
+                assert rx["rx_batched_answers"] == got["tx_frames"]  # every check the receiver made
+        got = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, 4096, 32], gpu))
+        assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+        assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["tx_frames"] + got["rx_frames"]
+        rx = got["batch"][1]
+        assert rx["rx_max_batch"] == 32 and rx["direct_answers"] == 0
+        _lib_counters_clean(got, gpu)
+    finally:
+        os.environ.pop("VAL_HARNESS_PARTIAL", None)

@@ -57,6 +57,8 @@ struct val_batch {
     size_t owe;
     uint8_t hdr_part[8];
     size_t hdr_have;
+    uint32_t cur_len;  /* CRC input of the frame in progress (its header is complete) */
+    uint32_t (*ticks)(void);  /* the config's clock (val_config_t.system.get_ticks_ms), for read deadlines */
     int raw;  /* a header announced content beyond the MTU: no more read-ahead */
     /* delivery of frame rx_cur into recv_buffer in place */
     size_t cur_matched;
@@ -212,10 +214,12 @@ static size_t vb_content_max(const val_batch_t *b)
     return b->mtu - VAL_WIRE_HEADER_SIZE - VAL_WIRE_TRAILER_SIZE;
 }
 
-/* Refill the empty ring: the frame in progress (or the next one, waiting up
- * to timeout_ms for its first byte), then every further frame the transport
- * already holds. Complete frames are hashed in one batch. Returns 0, or -1
- * on a transport error. */
+/* Refill the empty ring: the frame in progress (or the next one), for which
+ * the transport is given up to timeout_ms as the session would give it (over
+ * as many partial reads as it takes), then every further byte the transport
+ * already holds (zero-timeout polls, until one returns nothing). Complete
+ * frames that began in this ring are hashed in one batch. Returns 0, or -1 on
+ * a transport error. */
 static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
 {
     b->r_base += b->r_len;
@@ -223,59 +227,58 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     b->rx_n = b->rx_cur = 0;
     const size_t cap = b->opt.max_bytes;
     if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
+    const uint32_t t0 = b->ticks ? b->ticks() : 0u;
+    /* a frame carried over from the previous ring is delivered, not batched */
+    int whole = b->hdr_have == 0 && b->owe == 0;
+    uint64_t fstart = 0;
     int first = 1;
     for (;;) {
-        if (b->owe == 0) {
-            /* at a frame boundary: the next header */
-            if (b->rx_n >= b->opt.max_frames || cap - b->r_len < b->mtu) break;
-            const uint32_t t = first ? timeout_ms : 0u;
-            long g = vb_read(b, b->hdr_part + b->hdr_have, VAL_WIRE_HEADER_SIZE - b->hdr_have, t);
+        uint32_t budget = 0;  /* frames read ahead: only what is there */
+        if (first) {
+            const uint32_t el = b->ticks ? b->ticks() - t0 : 0u;
+            budget = timeout_ms > el ? timeout_ms - el : 0u;
+        }
+        if (b->owe == 0) {  /* the header */
+            if (b->hdr_have == 0) {
+                if (b->rx_n >= b->opt.max_frames || cap - b->r_len < b->mtu) break;
+                fstart = b->r_len;
+            }
+            const long g = vb_read(b, b->hdr_part + b->hdr_have, VAL_WIRE_HEADER_SIZE - b->hdr_have, budget);
             if (g < 0) return -1;
-            if (g == 0 && b->hdr_have == 0) break;
-            const size_t start_have = b->hdr_have;
+            memcpy(b->rx + b->r_len, b->hdr_part + b->hdr_have, (size_t)g);
+            b->r_len += (size_t)g;
             b->hdr_have += (size_t)g;
             if (b->hdr_have < VAL_WIRE_HEADER_SIZE) {
-                /* a partial header: the rest is owed (deliver what we have) */
-                memcpy(b->rx + b->r_len, b->hdr_part + start_have, (size_t)g);
-                b->r_len += (size_t)g;
+                if (g > 0 && (!first || budget > 0)) continue;  /* partial read: more may be there */
                 break;
             }
             const size_t content = (size_t)b->hdr_part[2] | (size_t)b->hdr_part[3] << 8;
-            memcpy(b->rx + b->r_len, b->hdr_part + start_have, VAL_WIRE_HEADER_SIZE - start_have);
-            const uint64_t fstart = b->r_len - start_have;  /* may lie before this ring (partial header) */
-            b->r_len += VAL_WIRE_HEADER_SIZE - start_have;
-            b->hdr_have = 0;
             if (content > vb_content_max(b)) {
                 /* the session will reject it (src/val_core.c:915-921); the
                    stream has no trustworthy boundaries after this */
                 b->raw = 1;
                 break;
             }
+            b->cur_len = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
             b->owe = content + VAL_WIRE_TRAILER_SIZE;
-            /* the asked-for frame waits as the session would; a frame read
-               ahead takes only what is there already, so the frames before it
-               are not held back by a late body */
-            const long r = vb_read(b, b->rx + b->r_len, b->owe, first ? timeout_ms : 0u);
-            if (r < 0) return -1;
-            b->r_len += (size_t)r;
-            b->owe -= (size_t)r;
-            if (b->owe) break;  /* the rest is late: stop reading ahead */
-            if (start_have == 0) {
-                vb_frame_t *f = &b->rxf[b->rx_n++];
-                f->off = fstart;
-                f->len = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
-                f->need = 1;
-            }
-            first = 0;
-        } else {
-            /* the rest of a frame that began in the previous ring */
-            const long r = vb_read(b, b->rx + b->r_len, b->owe, timeout_ms);
-            if (r < 0) return -1;
-            b->r_len += (size_t)r;
-            b->owe -= (size_t)r;
-            if (b->owe || r == 0) break;
-            first = 0;
         }
+        const long r = vb_read(b, b->rx + b->r_len, b->owe, budget);
+        if (r < 0) return -1;
+        b->r_len += (size_t)r;
+        b->owe -= (size_t)r;
+        if (b->owe) {
+            if (r > 0 && (!first || budget > 0)) continue;
+            break;
+        }
+        if (whole) {  /* complete, and every byte of it is in this ring */
+            vb_frame_t *f = &b->rxf[b->rx_n++];
+            f->off = fstart;
+            f->len = b->cur_len;
+            f->need = 1;
+        }
+        b->hdr_have = 0;
+        whole = 1;
+        first = 0;
     }
     if (b->rx_n) {
         const val_status_t st = vb_hash(b, b->rx, b->r_len, b->rxf, b->rx_n, 0);
@@ -426,6 +429,7 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     b->u_flush = cfg->transport.flush;
     b->u_io = cfg->transport.io_context;
     b->u_provider = cfg->crc32_provider;
+    b->ticks = cfg->system.get_ticks_ms;
     b->send_buffer = (const uint8_t *)cfg->buffers.send_buffer;
     b->recv_buffer = (const uint8_t *)cfg->buffers.recv_buffer;
     b->pinned = val_gpu_device_count() > 0;  /* pinned windows: DMA in place on the GPU path */
