@@ -70,16 +70,19 @@ struct val_batch {
     uint32_t *len_tmp;
 };
 
-static val_batch_t *volatile g_reg[VB_MAX_ATTACHED];
+/* The attached sessions: a slot's buffers are compared without touching its
+ * batcher, so a provider call never dereferences another session's batcher
+ * (which its own thread may be detaching and freeing). A buffer that matches
+ * is the calling session's own, and so is the batcher in that slot. */
+static val_batch_t *g_reg[VB_MAX_ATTACHED];
+static const void *g_buf[2][VB_MAX_ATTACHED];  /* [0]: send_buffer, [1]: recv_buffer */
 static int g_hwm;  /* slots [0, g_hwm) have been used: the provider scans only those */
 
 static val_batch_t *vb_lookup(const void *buf, int rx)
 {
     const int hwm = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
-    for (int i = 0; i < hwm; i++) {
-        val_batch_t *b = __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
-        if (b && (rx ? (const void *)b->recv_buffer : (const void *)b->send_buffer) == buf) return b;
-    }
+    for (int i = 0; i < hwm; i++)
+        if (__atomic_load_n(&g_buf[rx][i], __ATOMIC_ACQUIRE) == buf) return __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
     return NULL;
 }
 
@@ -399,6 +402,14 @@ static void vb_free(void *p, int pinned)
     else free(p);
 }
 
+/* buffers first, so no lookup matches a slot whose batcher is going */
+static void vb_release_slot(int i)
+{
+    __atomic_store_n(&g_buf[0][i], NULL, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_buf[1][i], NULL, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_reg[i], NULL, __ATOMIC_RELEASE);
+}
+
 val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out)
 {
     if (!cfg || !out || !cfg->transport.send || !cfg->transport.recv || !cfg->buffers.send_buffer ||
@@ -447,12 +458,14 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
         if (__atomic_compare_exchange_n(&g_reg[i], &expect, b, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) slot = i;
     }
     if (slot >= 0) {
+        __atomic_store_n(&g_buf[0][slot], (const void *)b->send_buffer, __ATOMIC_RELEASE);
+        __atomic_store_n(&g_buf[1][slot], (const void *)b->recv_buffer, __ATOMIC_RELEASE);
         int h = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
         while (h < slot + 1 && !__atomic_compare_exchange_n(&g_hwm, &h, slot + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
         }
     }
     if (!b->tx || !b->rx || !b->txf || !b->rxf || !b->crc_tmp || !b->off_tmp || !b->len_tmp || slot < 0) {
-        if (slot >= 0) __atomic_store_n(&g_reg[slot], NULL, __ATOMIC_RELEASE);
+        if (slot >= 0) vb_release_slot(slot);
         vb_free(b->tx, b->tx_pinned);
         vb_free(b->rx, b->rx_pinned);
         free(b->txf);
@@ -493,10 +506,11 @@ void val_batch_detach(val_batch_t *b)
 {
     if (!b) return;
     (void)vb_flush_tx(b);
-    for (int i = 0; i < VB_MAX_ATTACHED; i++) {
-        val_batch_t *expect = b;
-        if (__atomic_compare_exchange_n(&g_reg[i], &expect, NULL, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) break;
-    }
+    for (int i = 0; i < VB_MAX_ATTACHED; i++)
+        if (__atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE) == b) {
+            vb_release_slot(i);
+            break;
+        }
     val_config_t *cfg = b->cfg;
     cfg->transport.send = b->u_send;
     cfg->transport.recv = b->u_recv;
