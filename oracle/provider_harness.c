@@ -238,15 +238,8 @@ static int tp_send(void *ctx, const void *data, size_t len)
 /* VAL_HARNESS_PARTIAL=N: every transport.recv returns at most N bytes (and
  * whatever is there, once anything is): partial reads, which val_recv_full
  * (src/val_core.c:12-43) loops over. */
-static size_t partial_env(void)
-{
-    static long v = -1;
-    if (v < 0) {
-        const char *e = getenv("VAL_HARNESS_PARTIAL");
-        v = e ? (long)strtoul(e, NULL, 0) : 0;
-    }
-    return (size_t)v;
-}
+static size_t g_partial;  /* read once in main, before any session thread */
+static size_t partial_env(void) { return g_partial; }
 
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
 {
@@ -1348,6 +1341,9 @@ static int mode_sessions(crc32_func_t prov, int batched)
 
 int main(int argc, char **argv)
 {
+    const char *pe = getenv("VAL_HARNESS_PARTIAL");
+    g_partial = pe ? (size_t)strtoul(pe, NULL, 0) : 0;
+    (void)val_crc32_init_state();  /* the reference's lazy table (src/val_core.c:133-148), before any thread */
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions(NULL, 0);
     if (argc < 3) {

@@ -31,6 +31,7 @@ product's CPU counters must not move. The harness binary is built here and
 travels with the tree; where it is absent the tests skip."""
 import json
 import os
+import shutil
 import subprocess
 
 import pytest
@@ -244,3 +245,30 @@ def test_partial_read_transport(gpu):
         _lib_counters_clean(got, gpu)
     finally:
         os.environ.pop("VAL_HARNESS_PARTIAL", None)
+
+
+@needs_harness
+@pytest.mark.skipif(not os.path.isdir("/root/reference") or shutil.which("g++") is None,
+                    reason="the instrumented harness is built from /root/reference (build container only)")
+def test_batched_sessions_under_thread_sanitizer(tmp_path):
+    """ThreadSanitizer over four concurrent batched transfers (eight session
+    threads, one provider registry): every transfer ends clean and no report
+    has a frame in the product (val_batch.c, the library). Reports inside the
+    reference itself are expected and not ours (lazy table init,
+    src/val_core.c:133-148; a static debug counter, src/val_receiver.c:981-982)."""
+    vc.lib()
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "tsan_sessions.sh"), str(tmp_path)], capture_output=True,
+                       text=True, timeout=600, env=_env(False), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(out["runs"]) == 4 and out["lib_cpu_fallbacks"] == 0
+    for run in out["runs"]:
+        assert run["tx_status"] == VAL_OK and run["rx_status"] == VAL_OK and run["equal"] == 1, run
+        assert run["batch"][1]["rx_batched_answers"] >= 2_000_000 // (4096 - 12)
+    reports = (tmp_path / "tsan.txt").read_text().split("==================")
+    def ours(rep):  # a frame in the product, or a race whose access is in the harness (our checker)
+        top = [ln for ln in rep.splitlines() if ln.strip().startswith("#0")]
+        return "val_protocol_amd" in rep or "libval_tsan" in rep or any("provider_harness.c" in ln for ln in top)
+
+    ours = [rep for rep in reports if "WARNING: ThreadSanitizer" in rep and ours(rep)]
+    assert not ours, ours[0][:3000]
