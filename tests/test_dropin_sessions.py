@@ -250,25 +250,35 @@ def test_partial_read_transport(gpu):
 @needs_harness
 @pytest.mark.skipif(not os.path.isdir("/root/reference") or shutil.which("g++") is None,
                     reason="the instrumented harness is built from /root/reference (build container only)")
-def test_batched_sessions_under_thread_sanitizer(tmp_path):
+@pytest.mark.parametrize("mode", ["tsan", "asan"])
+def test_batched_sessions_under_sanitizers(tmp_path, mode):
     """ThreadSanitizer over four concurrent batched transfers (eight session
-    threads, one provider registry): every transfer ends clean and no report
-    has a frame in the product (val_batch.c, the library). Reports inside the
-    reference itself are expected and not ours (lazy table init,
-    src/val_core.c:133-148; a static debug counter, src/val_receiver.c:981-982)."""
+    threads, one provider registry); AddressSanitizer + UBSan over a
+    partial-read batched transfer and the same four. Every transfer ends
+    clean, and no report has a frame in the product (val_batch.c, cpu_crc32.c,
+    the library) or an access in the harness. Reports inside the reference
+    itself are expected and not ours (a static debug counter,
+    src/val_receiver.c:981-982; unaligned u64/u32 stores, src/val_wire.c:126,137
+    and src/val_core.c:833)."""
     vc.lib()
-    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "tsan_sessions.sh"), str(tmp_path)], capture_output=True,
-                       text=True, timeout=600, env=_env(False), cwd=ROOT)
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "sanitize_sessions.sh"), mode, str(tmp_path)],
+                       capture_output=True, text=True, timeout=900, env=_env(False), cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert len(out["runs"]) == 4 and out["lib_cpu_fallbacks"] == 0
-    for run in out["runs"]:
+    lines = [json.loads(ln) for ln in r.stdout.strip().splitlines()]
+    par = lines[-1]
+    assert len(par["runs"]) == 4 and par["lib_cpu_fallbacks"] == 0
+    runs = par["runs"] + lines[:-1]
+    assert len(runs) == (5 if mode == "asan" else 4)
+    for run in runs:
         assert run["tx_status"] == VAL_OK and run["rx_status"] == VAL_OK and run["equal"] == 1, run
-        assert run["batch"][1]["rx_batched_answers"] >= 2_000_000 // (4096 - 12)
-    reports = (tmp_path / "tsan.txt").read_text().split("==================")
-    def ours(rep):  # a frame in the product, or a race whose access is in the harness (our checker)
-        top = [ln for ln in rep.splitlines() if ln.strip().startswith("#0")]
-        return "val_protocol_amd" in rep or "libval_tsan" in rep or any("provider_harness.c" in ln for ln in top)
+        assert run["batch"][1]["rx_batched_answers"] >= (1 << 20) // (4096 - 12)
 
-    ours = [rep for rep in reports if "WARNING: ThreadSanitizer" in rep and ours(rep)]
-    assert not ours, ours[0][:3000]
+    def ours(rep):  # a frame in the product, or an access whose top frame is in the harness (our checker)
+        top = [ln for ln in rep.splitlines() if ln.strip().startswith("#0")]
+        return ("val_protocol_amd" in rep or "libval_san" in rep or any("provider_harness.c" in ln for ln in top))
+
+    text = (tmp_path / "report.txt").read_text()
+    reports = [rep for rep in text.split("==================") if "Sanitizer" in rep] + \
+              [ln for ln in text.splitlines() if "runtime error" in ln]
+    found = [rep for rep in reports if ours(rep)]
+    assert not found, found[0][:3000]
