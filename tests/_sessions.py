@@ -89,9 +89,8 @@ def control(s, lib):
         assert len(recs) == 1, (ptype, size, len(recs))
         return (ctypes.c_uint8 * size).from_buffer_copy(bytes.fromhex(recs[0][4])[8:])
 
-    lib.val_deserialize_resume_resp.argtypes = [ctypes.c_void_p, ctypes.POINTER(ResumeResp)]
-    lib.val_deserialize_verify_request.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 3
-    lib.val_deserialize_verify_response.argtypes = [ctypes.c_void_p] * 3
+    # every argument is a pointer and passed as one; no argtypes are set on the
+    # shared library object, so other tests' calls are unaffected
     rr = ResumeResp()
     lib.val_deserialize_resume_resp(payload(s["rx_frames"], PKT_RESUME_RESP, 24), ctypes.byref(rr))
     off, crc, ln = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
