@@ -239,6 +239,7 @@ static int tp_send(void *ctx, const void *data, size_t len)
  * whatever is there, once anything is): partial reads, which val_recv_full
  * (src/val_core.c:12-43) loops over. */
 static size_t g_partial;  /* read once in main, before any session thread */
+static int g_coalesce;    /* VAL_HARNESS_COALESCE=1: the batcher's coalesce_send (one send per window) */
 static size_t partial_env(void) { return g_partial; }
 
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
@@ -418,7 +419,7 @@ static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
 {
     fn_battach_t at = (fn_battach_t)dlsym(g_lib, "val_batch_attach");
     if (!at) return -1;
-    hb_opts_t o = {0, 0, 1, 1, 0};
+    hb_opts_t o = {0, 0, 1, 1, g_coalesce};
     if (at(a, &o, ba) != 0 || at(b, &o, bb) != 0) return -1;
     return 0;
 }
@@ -708,17 +709,27 @@ static void *rx_main(void *arg)
 }
 
 /* Every frame an end put on the wire carries the reference's own CRC
- * (val_crc32 of this binary) as its trailer: counted over the frame log. */
-static unsigned long trailers_ok(const end_t *e)
+ * (val_crc32 of this binary) as its trailer: counted over the frame log. A
+ * logged send may hold several frames back to back (the batcher's
+ * coalesce_send): they are split by their headers' content_len. */
+static unsigned long trailers_ok_n(const end_t *e, unsigned long *frames)
 {
-    unsigned long n = 0;
+    unsigned long n = 0, k = 0;
     for (size_t i = 0; i < e->nlog; i++) {
         const uint8_t *f = e->log[i].bytes;
         const size_t wl = e->log[i].len;
-        n += wl >= 12 && val_crc32(f, wl - 4) == le32(f + wl - 4);
+        for (size_t pos = 0; pos + 12 <= wl;) {
+            const size_t fl = 12u + (size_t)(f[pos + 2] | f[pos + 3] << 8);
+            const size_t use = fl <= wl - pos ? fl : wl - pos;
+            n += val_crc32(f + pos, use - 4) == le32(f + pos + use - 4);
+            k++;
+            pos += use;
+        }
     }
+    if (frames) *frames = k;
     return n;
 }
+static unsigned long trailers_ok(const end_t *e) { return trailers_ok_n(e, NULL); }
 
 static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, uint16_t window, int batched,
                         uint64_t seed)
@@ -773,6 +784,8 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     val_get_metrics(tx, &mt);
     val_get_metrics(rx, &mr);
     int equal = 0;
+    unsigned long wf_tx = 0, wf_rx = 0;
+    const unsigned long t_ok = trailers_ok_n(&etx, &wf_tx) + trailers_ok_n(&erx, &wf_rx);
     FILE *g = fopen(out, "rb");
     if (g) {
         uint8_t *back = (uint8_t *)malloc(bytes + 1);
@@ -784,11 +797,11 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     fprintf(out_json, "{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
            "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
-           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"flipped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"wire_frames\":%lu,\"flipped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
            "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
            use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
            mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
-           trailers_ok(&etx) + trailers_ok(&erx), etx.flipped, g_calls, t1 - t0,
+           t_ok, wf_tx + wf_rx, etx.flipped, g_calls, t1 - t0,
            (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
            (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
            (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
@@ -1343,6 +1356,8 @@ int main(int argc, char **argv)
 {
     const char *pe = getenv("VAL_HARNESS_PARTIAL");
     g_partial = pe ? (size_t)strtoul(pe, NULL, 0) : 0;
+    const char *ce = getenv("VAL_HARNESS_COALESCE");
+    g_coalesce = ce ? atoi(ce) : 0;
     (void)val_crc32_init_state();  /* the reference's lazy table (src/val_core.c:133-148), before any thread */
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions(NULL, 0);

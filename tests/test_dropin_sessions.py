@@ -248,6 +248,29 @@ def test_partial_read_transport(gpu):
 
 
 @needs_harness
+@pytest.mark.parametrize("gpu", MODES)
+def test_coalesced_window_sends(gpu):
+    """coalesce_send (include/val_batch.h): each window goes to the
+    application's transport as ONE send of its frames back to back. The
+    receiver's stream is unchanged (it reads frames by their headers,
+    src/val_core.c:880-945), the transfer ends clean, and every frame inside
+    every send carries the reference's own CRC."""
+    os.environ["VAL_HARNESS_COALESCE"] = "1"
+    try:
+        got = _line(_run([vc.LIB_PATH, "loopback-batched", 3 << 20, 16404, 64], gpu))
+    finally:
+        os.environ.pop("VAL_HARNESS_COALESCE", None)
+    assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+    assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"]
+    tx, rx = got["batch"]
+    assert tx["tx_max_batch"] == 64 and tx["tx_frames"] >= (3 << 20) // (16404 - 12)
+    assert got["tx_frames"] < tx["tx_frames"] // 8  # the sender's transport.send calls: one per window
+    assert got["wire_frames"] == tx["tx_frames"] + rx["tx_frames"]
+    assert rx["rx_batched_answers"] >= (3 << 20) // (16404 - 12)
+    _lib_counters_clean(got, gpu)
+
+
+@needs_harness
 @pytest.mark.skipif(not os.path.isdir("/root/reference") or shutil.which("g++") is None,
                     reason="the instrumented harness is built from /root/reference (build container only)")
 @pytest.mark.parametrize("mode", ["tsan", "asan"])
