@@ -36,12 +36,26 @@
  *       that frame's batch CRC. Every other provider call (resume windows,
  *       frames split across read-aheads) is computed directly.
  *
+ * When batching pays (VAL_BATCH_AUTO, the default): a batch only helps
+ * when it is large enough to run on the GPU. Below the host-batch crossover
+ * (val_gpu_host_batch_min_bytes) the CPU engine hashes a frame as fast alone
+ * as in a batch, and batching only costs time: the sender's frames wait for
+ * the end of the window fill, and a receiver that reads ahead holds its first
+ * frame until the rest of the window is in (measured on the reference's
+ * loopback at MTU 1,024 / window 64: read-ahead doubled the transfer time,
+ * deferred sends added 15-20%). So in AUTO a direction batches only when its
+ * largest possible batch, min(max_bytes, window_cap_packets x packet_size),
+ * reaches the crossover (checked at every window, so
+ * val_gpu_set_host_batch_min_bytes takes effect at once); otherwise TX frames
+ * get their trailer from the provider and go out at once, and RX reads only
+ * the frame the session asked for, whose check the provider computes. ALWAYS
+ * batches regardless (coalesce_send implies it for TX).
+ *
  * The application keeps its own transport and provider semantics: the
  * wrapped hooks call the ones in the config at attach time (a NULL provider
  * means this library's val_gpu_crc32_provider). Batches below the host-batch
- * crossover run on the CPU engine (val_gpu_host_batch_min_bytes), larger
- * ones on the GPU; VAL_GPU_HOST_BATCH_MIN_BYTES=0 sends every window to the
- * GPU.
+ * crossover run on the CPU engine, larger ones on the GPU;
+ * VAL_GPU_HOST_BATCH_MIN_BYTES=0 sends every window to the GPU.
  */
 #ifndef VAL_BATCH_H
 #define VAL_BATCH_H
@@ -56,11 +70,15 @@
 extern "C" {
 #endif
 
+#define VAL_BATCH_OFF 0     /* the reference's behaviour: the provider per frame */
+#define VAL_BATCH_AUTO 1    /* batch when a batch can reach the GPU (see above) */
+#define VAL_BATCH_ALWAYS 2  /* batch every window */
+
 typedef struct {
     uint32_t max_frames;  /* frames per batch, TX and RX (0 = 65,535) */
     size_t max_bytes;     /* wire bytes per batch (0 = 16 MiB; at least one MTU) */
-    int tx;               /* 1: defer TX trailers to window batches */
-    int rx;               /* 1: read ahead and hash RX frames in batches */
+    int tx;               /* VAL_BATCH_*: defer TX trailers to window batches */
+    int rx;               /* VAL_BATCH_*: read ahead and hash RX frames in batches */
     int coalesce_send;    /* 1: one transport.send per flushed window (0: one per frame, as the reference) */
 } val_batch_opts_t;
 
@@ -82,7 +100,8 @@ typedef struct val_batch val_batch_t;
 /* Wrap cfg->transport and cfg->crc32_provider (cfg->buffers.send_buffer,
  * recv_buffer and packet_size must be set; the two buffers must differ and
  * not belong to another attached config: VAL_ERR_INVALID_ARG otherwise).
- * opts may be NULL (defaults: TX and RX batching on). Attach before
+ * opts may be NULL (defaults: VAL_BATCH_AUTO both ways; tx/rx outside
+ * VAL_BATCH_OFF..ALWAYS: VAL_ERR_INVALID_ARG). Attach before
  * val_session_create (the session copies the config); call val_batch_detach
  * after val_session_destroy. Up to 256 attached configs per process. */
 val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out);

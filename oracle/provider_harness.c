@@ -240,6 +240,10 @@ static int tp_send(void *ctx, const void *data, size_t len)
  * (src/val_core.c:12-43) loops over. */
 static size_t g_partial;  /* read once in main, before any session thread */
 static int g_coalesce;    /* VAL_HARNESS_COALESCE=1: the batcher's coalesce_send (one send per window) */
+/* the batcher's modes (include/val_batch.h: 0 off, 1 auto, 2 always): always by
+   default, the mechanics under test; VAL_HARNESS_BATCH=tx|rx|none: one
+   direction or neither; VAL_HARNESS_BATCH_MODE=auto: the library's default */
+static int g_batch_tx = 2, g_batch_rx = 2;
 static size_t partial_env(void) { return g_partial; }
 
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
@@ -419,8 +423,11 @@ static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
 {
     fn_battach_t at = (fn_battach_t)dlsym(g_lib, "val_batch_attach");
     if (!at) return -1;
-    hb_opts_t o = {0, 0, 1, 1, g_coalesce};
-    if (at(a, &o, ba) != 0 || at(b, &o, bb) != 0) return -1;
+    hb_opts_t o = {0, 0, g_batch_tx, g_batch_rx, g_coalesce};
+    if (getenv("VAL_HARNESS_BATCH_FRAMES")) o.max_frames = (uint32_t)atoi(getenv("VAL_HARNESS_BATCH_FRAMES"));
+    const char *only = getenv("VAL_HARNESS_BATCH_END");  /* sender|receiver: attach one end only */
+    if ((!only || strcmp(only, "receiver")) && at(a, &o, ba) != 0) return -1;
+    if ((!only || strcmp(only, "sender")) && at(b, &o, bb) != 0) return -1;
     return 0;
 }
 
@@ -801,7 +808,7 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
            "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
            use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
            mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
-           t_ok, wf_tx + wf_rx, etx.flipped, g_calls, t1 - t0,
+           t_ok, wf_tx + wf_rx, etx.flipped, __atomic_load_n(&g_calls, __ATOMIC_RELAXED), t1 - t0,
            (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
            (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
            (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
@@ -1358,6 +1365,15 @@ int main(int argc, char **argv)
     g_partial = pe ? (size_t)strtoul(pe, NULL, 0) : 0;
     const char *ce = getenv("VAL_HARNESS_COALESCE");
     g_coalesce = ce ? atoi(ce) : 0;
+    const char *be = getenv("VAL_HARNESS_BATCH");
+    if (be && !strcmp(be, "tx")) g_batch_rx = 0;
+    if (be && !strcmp(be, "rx")) g_batch_tx = 0;
+    if (be && !strcmp(be, "none")) g_batch_tx = g_batch_rx = 0;
+    const char *bm = getenv("VAL_HARNESS_BATCH_MODE");
+    if (bm && !strcmp(bm, "auto")) {
+        g_batch_tx = g_batch_tx ? 1 : 0;
+        g_batch_rx = g_batch_rx ? 1 : 0;
+    }
     (void)val_crc32_init_state();  /* the reference's lazy table (src/val_core.c:133-148), before any thread */
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "fixtures")) return mode_fixtures();
     if (argc >= 3 && !strcmp(argv[1], "none") && !strcmp(argv[2], "sessions")) return mode_sessions(NULL, 0);

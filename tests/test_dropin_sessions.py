@@ -97,7 +97,7 @@ def test_loopback_with_product_provider_equals_reference(gpu):
         if mode[0] == "loopback-batched":
             tx, rx = got["batch"]
             assert tx["status"] == VAL_OK and rx["status"] == VAL_OK
-            assert tx["tx_batched_frames"] == 1045 + 5  # every frame the sender built (1,045 DATA + control)
+            assert tx["tx_batched_frames"] == 1045  # every DATA frame the sender built (control frames: direct)
             assert rx["rx_batched_answers"] >= 1045  # the receiver's checks, answered from its batches
         else:
             assert got["provider_calls"] >= got["tx_frames"] + got["rx_frames"]
@@ -235,16 +235,47 @@ def test_partial_read_transport(gpu):
                 _lib_counters_clean(got, gpu)
             if mode[1] == "loopback-batched":
                 rx = got["batch"][1]
-                assert rx["status"] == VAL_OK and rx["direct_answers"] == 0
-                assert rx["rx_batched_answers"] == got["tx_frames"]  # every check the receiver made
+                assert rx["status"] == VAL_OK and rx["rx_batched_answers"] == got["tx_frames"]  # every check it made
+                assert rx["direct_answers"] == got["rx_frames"]  # its own control frames' trailers only
         got = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, 4096, 32], gpu))
         assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
         assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["tx_frames"] + got["rx_frames"]
         rx = got["batch"][1]
-        assert rx["rx_max_batch"] == 32 and rx["direct_answers"] == 0
+        assert rx["rx_max_batch"] == 32 and rx["direct_answers"] == got["rx_frames"]
         _lib_counters_clean(got, gpu)
     finally:
         os.environ.pop("VAL_HARNESS_PARTIAL", None)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
+def test_auto_mode_batches_only_when_a_batch_can_reach_the_gpu(gpu):
+    """VAL_BATCH_AUTO, the attach default (include/val_batch.h, "When batching
+    pays"): with the library's own crossover (CPU variant: a window of 64 x
+    1,024 B can never reach 64 MiB) both ends pass frames straight through and
+    the provider answers every check; the wire of the window-1 loopback still
+    equals the reference's (F6 digests). With the crossover at 0 (GPU variant:
+    conftest forces every batch onto the GPU) the same windows batch."""
+    with open(os.path.join(ROOT, "tests", "golden", "dropin_vectors.json")) as f:
+        f6 = json.load(f)["loopback"]
+    os.environ["VAL_HARNESS_BATCH_MODE"] = "auto"
+    try:
+        one = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, 1024, 0], gpu))
+        win = _line(_run([vc.LIB_PATH, "loopback-batched", 4 << 20, 1024, 64], gpu))
+    finally:
+        os.environ.pop("VAL_HARNESS_BATCH_MODE", None)
+    assert one["tx_digest"] == f6["tx_digest"] and one["rx_digest"] == f6["rx_digest"]
+    for got in (one, win):
+        assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+        assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"]
+        _lib_counters_clean(got, gpu)
+    tx, rx = win["batch"]
+    if gpu:
+        assert tx["tx_max_batch"] == 64 and rx["rx_max_batch"] > 1 and rx["rx_batched_answers"] > 0
+    else:
+        for end in win["batch"] + one["batch"]:
+            assert end["tx_batches"] == 0 and end["rx_batches"] == 0 and end["rx_batched_answers"] == 0, end
+        assert rx["direct_answers"] == win["tx_frames"] + win["rx_frames"]  # every check and trailer, per frame
 
 
 @needs_harness

@@ -38,6 +38,7 @@ struct val_batch {
     val_batch_opts_t opt;
     const uint8_t *send_buffer, *recv_buffer;
     size_t mtu;
+    uint32_t win_cap;        /* the config's window cap in frames (0 in the config = 1, src/val_core.c:1755) */
     int pinned;              /* allocate windows pinned (a device is present) */
     int tx_pinned, rx_pinned; /* how each window buffer was allocated */
     /* TX window */
@@ -96,6 +97,22 @@ static uint32_t vb_direct(val_batch_t *b, uint32_t seed, const void *buf, size_t
 static void vb_fail(val_batch_t *b, val_status_t st)
 {
     if (b->st.status == VAL_OK) b->st.status = st;
+}
+
+/* Whether a direction batches now (include/val_batch.h, "When batching
+ * pays"): its largest possible batch against the host-batch crossover. */
+static int vb_engaged(const val_batch_t *b, int mode)
+{
+    if (mode == VAL_BATCH_ALWAYS) return 1;
+    if (mode != VAL_BATCH_AUTO) return 0;
+    uint64_t ub = (uint64_t)b->win_cap * b->mtu;
+    if (ub > b->opt.max_bytes) ub = b->opt.max_bytes;
+    return ub >= val_gpu_host_batch_min_bytes();
+}
+
+static int vb_tx_engaged(const val_batch_t *b)
+{
+    return b->opt.tx && (b->opt.coalesce_send || vb_engaged(b, b->opt.tx));
 }
 
 /* CRCs of frames f[0..n) of buf in one host batch call. */
@@ -165,7 +182,11 @@ static int vb_send(void *ctx, const void *data, size_t len)
     const size_t pending = b->tx_pending;
     b->tx_pending = 0;
     if (b->st.status != VAL_OK) return -1;
-    if (!b->opt.tx || len < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE || len > b->opt.max_bytes) {
+    /* the provider returned a placeholder for exactly this frame */
+    const int placeholder = data == (const void *)b->send_buffer && len >= VAL_WIRE_TRAILER_SIZE &&
+                            pending == len - VAL_WIRE_TRAILER_SIZE;
+    if (!b->opt.tx || len < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE || len > b->opt.max_bytes ||
+        (!placeholder && b->tx_n == 0 && !vb_tx_engaged(b))) {
         /* not a frame this batcher stages: send the window before it, then it */
         if (vb_flush_tx(b) != VAL_OK) return -1;
         const int rc = b->u_send(b->u_io, data, len);
@@ -177,8 +198,7 @@ static int vb_send(void *ctx, const void *data, size_t len)
     vb_frame_t *f = &b->txf[b->tx_n++];
     f->off = b->tx_used;
     f->len = (uint32_t)(len - VAL_WIRE_TRAILER_SIZE);
-    /* the provider returned a placeholder for exactly this frame */
-    f->need = (uint8_t)(data == (const void *)b->send_buffer && pending == f->len);
+    f->need = (uint8_t)placeholder;
     memcpy(b->tx + b->tx_used, data, len);
     b->tx_used += len;
     const uint8_t type = ((const uint8_t *)data)[0];
@@ -231,6 +251,11 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     const size_t cap = b->opt.max_bytes;
     if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
     const uint32_t t0 = b->ticks ? b->ticks() : 0u;
+    /* not batching now: the frame the session asked for only, its check left
+       to the provider */
+    const int eng = vb_engaged(b, b->opt.rx);
+    const uint32_t lim = eng ? b->opt.max_frames : 1u;
+    uint32_t nread = 0;
     /* a frame carried over from the previous ring is delivered, not batched */
     int whole = b->hdr_have == 0 && b->owe == 0;
     uint64_t fstart = 0;
@@ -243,7 +268,7 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
         }
         if (b->owe == 0) {  /* the header */
             if (b->hdr_have == 0) {
-                if (b->rx_n >= b->opt.max_frames || cap - b->r_len < b->mtu) break;
+                if (nread >= lim || cap - b->r_len < b->mtu) break;
                 fstart = b->r_len;
             }
             const long g = vb_read(b, b->hdr_part + b->hdr_have, VAL_WIRE_HEADER_SIZE - b->hdr_have, budget);
@@ -273,7 +298,8 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
             if (r > 0 && (!first || budget > 0)) continue;
             break;
         }
-        if (whole) {  /* complete, and every byte of it is in this ring */
+        nread += whole;
+        if (whole && eng) {  /* complete, and every byte of it is in this ring */
             vb_frame_t *f = &b->rxf[b->rx_n++];
             f->off = fstart;
             f->len = b->cur_len;
@@ -371,8 +397,12 @@ uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
 {
     val_batch_t *b = vb_lookup(buf, 0);
     if (b) {
-        if (b->opt.tx && seed == 0xFFFFFFFFu && b->st.status == VAL_OK) {
-            /* a TX frame in send_buffer: its trailer comes from the window batch */
+        /* a DATA frame (its type byte leads the header, src/val_core.c:828-835)
+           while batching: the trailer comes later from the window batch;
+           control frames (ACK, DONE, ...) go out alone at once, so they are
+           computed here */
+        if (seed == 0xFFFFFFFFu && len && ((const uint8_t *)buf)[0] == VAL_PKT_DATA && b->st.status == VAL_OK &&
+            vb_tx_engaged(b)) {
             b->tx_pending = len;
             return 0u;
         }
@@ -426,12 +456,17 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     if (!b) return VAL_ERR_NO_MEMORY;
     if (opts) b->opt = *opts;
     else {
-        b->opt.tx = 1;
-        b->opt.rx = 1;
+        b->opt.tx = VAL_BATCH_AUTO;
+        b->opt.rx = VAL_BATCH_AUTO;
+    }
+    if ((unsigned)b->opt.tx > VAL_BATCH_ALWAYS || (unsigned)b->opt.rx > VAL_BATCH_ALWAYS) {
+        free(b);
+        return VAL_ERR_INVALID_ARG;
     }
     if (!b->opt.max_frames) b->opt.max_frames = VB_DEFAULT_FRAMES;
     if (!b->opt.max_bytes) b->opt.max_bytes = VB_DEFAULT_BYTES;
     b->mtu = cfg->buffers.packet_size;
+    b->win_cap = cfg->tx_flow.window_cap_packets ? cfg->tx_flow.window_cap_packets : 1u;
     if (b->opt.max_bytes < b->mtu) b->opt.max_bytes = b->mtu;
     b->cfg = cfg;
     b->u_send = cfg->transport.send;
