@@ -194,6 +194,7 @@ typedef struct {
     size_t nlog, caplog;
     unsigned long recvs;  /* transport.recv calls of this end: frames sent between two are one window fill */
     unsigned long flip_every, data_sent, flipped;  /* fault injection: one payload bit of every Nth DATA frame */
+    uint64_t rng;  /* partial-read sizes (VAL_HARNESS_PARTIAL=rN) */
 } end_t;
 
 /* VAL_HARNESS_FLIP_EVERY=N: the sender's pipe flips one payload bit of every
@@ -244,14 +245,22 @@ static int g_coalesce;    /* VAL_HARNESS_COALESCE=1: the batcher's coalesce_send
    default, the mechanics under test; VAL_HARNESS_BATCH=tx|rx|none: one
    direction or neither; VAL_HARNESS_BATCH_MODE=auto: the library's default */
 static int g_batch_tx = 2, g_batch_rx = 2;
+static uint64_t g_seed;     /* VAL_HARNESS_SEED: partial-read draws */
+static int g_partial_random;  /* VAL_HARNESS_PARTIAL=rN: each recv returns 1..N bytes, drawn per call */
 static size_t partial_env(void) { return g_partial; }
+static size_t partial_draw(end_t *e)
+{
+    if (!g_partial_random) return g_partial;
+    e->rng = e->rng * 6364136223846793005ull + 1442695040888963407ull;  /* per-end LCG: no shared state */
+    return 1u + (size_t)((e->rng >> 33) % g_partial);
+}
 
 static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t timeout_ms)
 {
     end_t *e = (end_t *)ctx;
     e->recvs++;
     if (partial_env()) {
-        const size_t n = pipe_pop_upto(e->in, (uint8_t *)buffer, size, timeout_ms, partial_env());
+        const size_t n = pipe_pop_upto(e->in, (uint8_t *)buffer, size, timeout_ms, partial_draw(e));
         if (got) *got = n;
         return 0;
     }
@@ -763,6 +772,8 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
     erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
     etx.flip_every = flip_every_env();
+    etx.rng = g_seed * 2u + 1u;  /* partial-read draws (VAL_HARNESS_PARTIAL=rN), per end */
+    erx.rng = g_seed * 2u + 2u;
     crc32_func_t prov = use_gpu ? counting_provider : NULL;
     val_config_t ctx_, crx;
     make_cfg(&ctx_, &etx, mtu, prov);
@@ -1362,7 +1373,9 @@ static int mode_sessions(crc32_func_t prov, int batched)
 int main(int argc, char **argv)
 {
     const char *pe = getenv("VAL_HARNESS_PARTIAL");
-    g_partial = pe ? (size_t)strtoul(pe, NULL, 0) : 0;
+    g_partial_random = pe && pe[0] == 'r';
+    g_seed = getenv("VAL_HARNESS_SEED") ? strtoull(getenv("VAL_HARNESS_SEED"), NULL, 0) : 0u;
+    g_partial = pe ? (size_t)strtoul(pe + g_partial_random, NULL, 0) : 0;
     const char *ce = getenv("VAL_HARNESS_COALESCE");
     g_coalesce = ce ? atoi(ce) : 0;
     const char *be = getenv("VAL_HARNESS_BATCH");

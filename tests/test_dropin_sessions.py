@@ -249,6 +249,43 @@ def test_partial_read_transport(gpu):
 
 @needs_harness
 @pytest.mark.parametrize("gpu", MODES)
+def test_random_short_reads_fuzz(gpu):
+    """Seeded fuzz of the read-ahead's stream parser: recv returns a random
+    1..N bytes per call (VAL_HARNESS_PARTIAL=rN, a per-end generator seeded
+    by VAL_HARNESS_SEED), over MTUs 1,024..65,536 and windows 1, 4 and 32.
+    Every batched transfer ends clean, equal, with every trailer on the wire
+    the reference's. Then bit flips on top (every 50th DATA frame) at window 1:
+    the batched run rejects and retransmits exactly as the reference's own
+    built-in-CRC run does, with the same wire digests."""
+    for seed in range(1, 13):
+        part, window, mtu = f"r{seed * 977 % 5000 + 1}", (0, 4, 32)[seed % 3], (1024, 4096, 16404, 65536)[seed % 4]
+        os.environ.update(VAL_HARNESS_SEED=str(seed), VAL_HARNESS_PARTIAL=part)
+        try:
+            got = _line(_run([vc.LIB_PATH, "loopback-batched", 1_500_000, mtu, window], gpu))
+        finally:
+            for k in ("VAL_HARNESS_SEED", "VAL_HARNESS_PARTIAL"):
+                os.environ.pop(k, None)
+        case = (seed, part, window, mtu)
+        assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, (case, got)
+        assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"], case
+        assert got["batch"][1]["rx_batched_answers"] > 0, case
+        _lib_counters_clean(got, gpu)
+    env = dict(VAL_HARNESS_SEED="3", VAL_HARNESS_PARTIAL="r2932", VAL_HARNESS_FLIP_EVERY="50")
+    os.environ.update(env)
+    try:
+        ref = _line(_run(["none", "loopback", 1 << 20, 1024], gpu))
+        got = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, 1024, 0], gpu))
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    assert ref["flipped"] > 10 and ref["rx_crc_errors"] == ref["flipped"] and ref["equal"] == 1, ref
+    for k in ("tx_status", "rx_status", "equal", "rx_crc_errors", "retransmits", "flipped", "tx_digest", "rx_digest"):
+        assert got[k] == ref[k], (k, got[k], ref[k])
+    _lib_counters_clean(got, gpu)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
 def test_auto_mode_batches_only_when_a_batch_can_reach_the_gpu(gpu):
     """VAL_BATCH_AUTO, the attach default (include/val_batch.h, "When batching
     pays"): with the library's own crossover (CPU variant: a window of 64 x

@@ -6,7 +6,8 @@
 #         sharing the provider registry)
 #   asan: AddressSanitizer + UndefinedBehaviorSanitizer (the CPU engine
 #         cpu_crc32.c instrumented as well), one batched transfer at window 32
-#         over a transport that returns at most 7 bytes per recv, then four at once
+#         over a transport whose recv returns 1..3000 bytes (random per call),
+#         then four at once
 # usage: bash tools/sanitize_sessions.sh tsan|asan OUTDIR   (needs /root/reference
 # and a built library). Prints the harness's JSON lines; the sanitizers'
 # reports go to OUTDIR/report.txt.
@@ -32,7 +33,7 @@ gcc -O1 -g -std=gnu99 -w $SAN -DVAL_ENABLE_METRICS=1 -DVAL_LOG_LEVEL=0 -I"$REF/i
 export TSAN_OPTIONS="exitcode=0 log_path=$O/san" ASAN_OPTIONS="detect_leaks=0 log_path=$O/san" \
        UBSAN_OPTIONS="print_stacktrace=1 log_path=$O/san"
 if [ "$MODE" = asan ]; then
-  VAL_HARNESS_PARTIAL=7 "$O/harness" "$O/libval_san.so" loopback-batched 1048576 4096 32 2>> "$O/stderr.txt" | tail -1
+  VAL_HARNESS_PARTIAL=r3000 VAL_HARNESS_SEED=7 "$O/harness" "$O/libval_san.so" loopback-batched 1048576 4096 32 2>> "$O/stderr.txt" | tail -1
 fi
 "$O/harness" "$O/libval_san.so" loopback-batched-par 2000000 4096 32 4 2>> "$O/stderr.txt" | tail -1
 cat "$O"/san.[0-9]* "$O/stderr.txt" > "$O/report.txt" 2>/dev/null || :
