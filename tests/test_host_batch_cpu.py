@@ -196,3 +196,39 @@ def test_threshold_knob():
     vc.set_host_batch_min_bytes(-1)
     # the suite's conftest exports VAL_GPU_HOST_BATCH_MIN_BYTES=0 before the library loads
     assert vc.host_batch_min_bytes() == int(os.environ.get("VAL_GPU_HOST_BATCH_MIN_BYTES", vc.host_batch_min_bytes()))
+
+
+CHECK = os.path.join(ROOT, "oracle", "host_runtime_check")
+
+
+@pytest.mark.parametrize("gpu", [pytest.param(False, id="cpu_engine"), pytest.param(True, id="gpu", marks=pytest.mark.gpu)])
+def test_host_runtime_threads_of_random_batches(gpu):
+    """oracle/host_runtime_check (checker, built by `make -C oracle oracle`):
+    four threads at once, each with random packed unaligned batches of up to
+    3,000 frames and ~49 MiB, through val_crc32_frames_host,
+    val_crc32_verify_frames_ex_host (every 97th trailer corrupted; ok flags,
+    nbad, payload states), val_crc32_frames_host_multi (8 shards),
+    val_crc32_region_host_multi and the scalar hooks, every output against the
+    oracle. CPU variant: the library's thresholds with the CPU engine's helper
+    threads on (4 per call). GPU variant: thresholds at 0, so every call of
+    every thread goes through the GPU host path at once. The same program
+    under AddressSanitizer/UBSan and ThreadSanitizer: tools/
+    sanitize_host_runtime.sh (profiles/r05_sanitize_host_runtime.txt)."""
+    import subprocess
+
+    if not os.path.exists(CHECK):
+        pytest.skip("oracle/host_runtime_check not built (make -C oracle oracle)")
+    env = dict(os.environ)
+    if gpu:
+        env.update(VAL_GPU_HOST_BATCH_MIN_BYTES="0", VAL_GPU_PROVIDER_MIN_BYTES="0")
+    else:
+        env.pop("VAL_GPU_HOST_BATCH_MIN_BYTES", None)
+        env.pop("VAL_GPU_PROVIDER_MIN_BYTES", None)
+    r = subprocess.run([CHECK, "4", "6", "11"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["bad"] == 0 and out["frames_checked"] > 20000 and out["cpu_fallbacks"] == 0, out
+    if gpu:
+        assert out["devices"] >= 1 and out["cpu_batches"] == 0, out
+    else:
+        assert out["cpu_batches"] >= 4 * 6 * 2, out
