@@ -81,7 +81,8 @@ def test_no_gpu_means_loud_failure_not_fallback():
 def test_batch_attach_argument_checks():
     """val_batch_attach (include/val_batch.h) refuses configs the provider
     could not tell apart: one buffer for both directions, or a buffer that
-    another attached config already uses; detach restores the hooks. No
+    another attached config already uses, and a tx/rx that is not a
+    VAL_BATCH_* mode; detach restores the hooks. No
     GPU needed (the window buffers are plain host memory then)."""
     src = r"""
     #include "val_batch.h"
@@ -111,7 +112,17 @@ def test_batch_attach_argument_checks():
         int restored = x.transport.send == snd && x.crc32_provider == NULL;
         int r4 = val_batch_attach(&y, NULL, &by);          /* b is free again */
         val_batch_detach(by);
-        printf("%d %d %d %d %d %d\n", r1, r2, hooked, r3, restored, r4);
+        val_batch_opts_t o;
+        memset(&o, 0, sizeof o);
+        o.tx = VAL_BATCH_ALWAYS + 1;                        /* not a mode */
+        y.transport.send = snd;
+        int r5 = val_batch_attach(&y, &o, &by);
+        o.tx = VAL_BATCH_ALWAYS;
+        o.rx = VAL_BATCH_OFF;
+        int r6 = val_batch_attach(&y, &o, &by);
+        val_batch_detach(by);
+        printf("%d %d %d %d %d %d %d %d %d\n", r1, r2, hooked, r3, restored, r4, r5, r6,
+               VAL_BATCH_OFF * 100 + VAL_BATCH_AUTO * 10 + VAL_BATCH_ALWAYS);
         return 0;
     }
     """
@@ -124,4 +135,5 @@ def test_batch_attach_argument_checks():
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{INC}", c, "-o", exe, f"-L{libdir}",
                         "-l:libval_crc_hip.so", f"-Wl,-rpath,{libdir}"], check=True)
         out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
-    assert [int(v) for v in out] == [vc.VAL_ERR_INVALID_ARG, 0, 1, vc.VAL_ERR_INVALID_ARG, 1, 0]
+    assert [int(v) for v in out] == [vc.VAL_ERR_INVALID_ARG, 0, 1, vc.VAL_ERR_INVALID_ARG, 1, 0,
+                                     vc.VAL_ERR_INVALID_ARG, 0, 12]
