@@ -36,20 +36,26 @@
  *       that frame's batch CRC. Every other provider call (resume windows,
  *       frames split across read-aheads) is computed directly.
  *
- * When batching pays (VAL_BATCH_AUTO, the default): a batch only helps
- * when it is large enough to run on the GPU. Below the host-batch crossover
- * (val_gpu_host_batch_min_bytes) the CPU engine hashes a frame as fast alone
- * as in a batch, and batching only costs time: the sender's frames wait for
- * the end of the window fill, and a receiver that reads ahead holds its first
- * frame until the rest of the window is in (measured on the reference's
- * loopback at MTU 1,024 / window 64: read-ahead doubled the transfer time,
- * deferred sends added 15-20%). So in AUTO a direction batches only when its
- * largest possible batch, min(max_bytes, window_cap_packets x packet_size),
- * reaches the crossover (checked at every window, so
- * val_gpu_set_host_batch_min_bytes takes effect at once); otherwise TX frames
- * get their trailer from the provider and go out at once, and RX reads only
- * the frame the session asked for, whose check the provider computes. ALWAYS
- * batches regardless (coalesce_send implies it for TX).
+ * When batching pays (VAL_BATCH_AUTO, the default): a batch makes the CRC
+ * faster only when it is large enough to run on the GPU. Below the host-batch
+ * crossover (val_gpu_host_batch_min_bytes) a batch runs on the same CPU
+ * engine the provider uses per frame, so batching cannot speed the CRC up; it
+ * only moves frames in time (the sender's frames wait for the end of the
+ * window fill, the receiver reads ahead). Measured on the reference's own
+ * loopback, that moved the transfer rate by -24% to +14% against the plain
+ * provider depending on window and direction. So in
+ * AUTO a direction batches only when its largest possible batch,
+ * min(max_bytes, window_cap_packets x packet_size), reaches the crossover
+ * (checked at every window, so val_gpu_set_host_batch_min_bytes takes effect
+ * at once); otherwise TX frames get their trailer from the provider and go
+ * out at once, and RX reads only the frame the session asked for, whose
+ * check the provider computes. ALWAYS batches regardless (coalesce_send
+ * implies it for TX).
+ *
+ * The read-ahead polls the transport with a zero timeout, so such a recv must
+ * return at once, as a non-blocking socket read does. A transport whose
+ * zero-timeout recv sleeps (a condition-variable wait on an already expired
+ * deadline took ~70 us in our harness) adds that to every read-ahead.
  *
  * The application keeps its own transport and provider semantics: the
  * wrapped hooks call the ones in the config at attach time (a NULL provider

@@ -139,7 +139,9 @@ static size_t pipe_pop_upto(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms
     pthread_mutex_lock(&p->mu);
     const size_t need = upto ? 1 : n;
     while (p->len < need) {
-        if (pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
+        /* timeout 0 is a poll: return at once, as a non-blocking socket does
+           (a timed wait on an expired deadline still sleeps ~50-100 us) */
+        if (!timeout_ms || pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
             pthread_mutex_unlock(&p->mu);
             return 0;
         }
@@ -166,7 +168,7 @@ static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
     if (dl.tv_nsec >= 1000000000L) { dl.tv_sec++; dl.tv_nsec -= 1000000000L; }
     pthread_mutex_lock(&p->mu);
     while (p->len < n) {
-        if (pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
+        if (!timeout_ms || pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {  /* timeout 0: a poll */
             pthread_mutex_unlock(&p->mu);
             return 0;
         }
