@@ -222,7 +222,7 @@ static int vb_is_connected(void *ctx)
 }
 
 /* ---- RX ---------------------------------------------------------------- */
-/* Read exactly n bytes into dst from the application's transport within
+/* Read up to n bytes into dst from the application's transport within
  * timeout (its recv may return fewer); returns the bytes read or -1. */
 static long vb_read(val_batch_t *b, uint8_t *dst, size_t n, uint32_t timeout_ms)
 {
