@@ -22,14 +22,15 @@
  *       frames go to the application's transport in order. The wire is the
  *       reference's, byte for byte; only the time of sending moves to the
  *       end of the window fill.
- *   RX: the wrapped transport.recv reads ahead: the frame the session asked
- *       for (over as many short reads as the transport returns, within the
- *       session's timeout, measured with config->system.get_ticks_ms) plus
- *       every further frame the transport already holds (polled with a zero
- *       timeout while polls return bytes), up to the window limits; no byte
- *       read is ever dropped (a frame cut off by a poll finishes in the next
- *       read-ahead and is delivered unbatched). It computes their
- *       CRCs with ONE val_crc32_frames_host call. It hands bytes to the
+ *   RX: (recv_polls, below) the wrapped transport.recv reads ahead: the
+ *       frame the session asked for (over as many short reads as the
+ *       transport returns, within the session's timeout, measured with
+ *       config->system.get_ticks_ms) plus every further frame the transport
+ *       already holds (polled with a zero timeout while polls return bytes),
+ *       up to the window limits; no byte read is ever dropped (a frame cut
+ *       off by a poll finishes in the next read-ahead and is delivered
+ *       unbatched). It computes their CRCs with ONE val_crc32_frames_host
+ *       call. It hands bytes to the
  *       session exactly as asked; when a frame's header and content were
  *       delivered to recv_buffer in place and its trailer after them, the
  *       provider call that follows (src/val_core.c:964) is answered with
@@ -52,10 +53,14 @@
  * check the provider computes. ALWAYS batches regardless (coalesce_send
  * implies it for TX).
  *
- * The read-ahead polls the transport with a zero timeout, so such a recv must
- * return at once, as a non-blocking socket read does. A transport whose
- * zero-timeout recv sleeps (a condition-variable wait on an already expired
- * deadline took ~70 us in our harness) adds that to every read-ahead.
+ * Reading ahead means polling the transport with a zero timeout. The
+ * reference's contract does not define timeout 0 (the reference itself never
+ * passes it, src/val_core.c:31) and its own TCP example blocks forever on it
+ * (examples/tcp/common/tcp_util.c:383), which would deadlock a read-ahead at
+ * the end of every window. So RX reads ahead only when the application says
+ * its recv polls (recv_polls = 1). Such a poll must also be cheap: a
+ * condition-variable wait on an already expired deadline took ~70 us per
+ * empty poll in our harness and added that to every read-ahead.
  *
  * The application keeps its own transport and provider semantics: the
  * wrapped hooks call the ones in the config at attach time (a NULL provider
@@ -86,6 +91,10 @@ typedef struct {
     int tx;               /* VAL_BATCH_*: defer TX trailers to window batches */
     int rx;               /* VAL_BATCH_*: read ahead and hash RX frames in batches */
     int coalesce_send;    /* 1: one transport.send per flushed window (0: one per frame, as the reference) */
+    int recv_polls;       /* 1: transport.recv with timeout 0 returns at once (nothing there: *received = 0), as a
+                             non-blocking socket read does; RX reads ahead only then. 0 (default): the reference's
+                             contract, where timeout 0 may block (its TCP example waits forever): RX reads only
+                             the frame the session asked for, and its checks come from the provider */
 } val_batch_opts_t;
 
 typedef struct {

@@ -93,6 +93,11 @@ static void delay(uint32_t ms)
 static uint32_t le32(const uint8_t *p);
 
 /* ---- in-memory byte pipe ------------------------------------------------ */
+/* VAL_HARNESS_ZERO_BLOCKS=1: recv with timeout 0 waits until the request can
+   be met, as the reference's TCP example does (examples/tcp/common/
+   tcp_util.c:383: select with no timeout) */
+static int g_zero_blocks;
+
 typedef struct {
     uint8_t *buf;
     size_t cap, head, len;
@@ -140,7 +145,12 @@ static size_t pipe_pop_upto(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms
     const size_t need = upto ? 1 : n;
     while (p->len < need) {
         /* timeout 0 is a poll: return at once, as a non-blocking socket does
-           (a timed wait on an expired deadline still sleeps ~50-100 us) */
+           (a timed wait on an expired deadline still sleeps ~50-100 us);
+           unless told to block, as the reference's TCP example does */
+        if (!timeout_ms && g_zero_blocks) {
+            pthread_cond_wait(&p->cv, &p->mu);
+            continue;
+        }
         if (!timeout_ms || pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {
             pthread_mutex_unlock(&p->mu);
             return 0;
@@ -168,6 +178,10 @@ static int pipe_pop(pipe_t *p, uint8_t *d, size_t n, uint32_t timeout_ms)
     if (dl.tv_nsec >= 1000000000L) { dl.tv_sec++; dl.tv_nsec -= 1000000000L; }
     pthread_mutex_lock(&p->mu);
     while (p->len < n) {
+        if (!timeout_ms && g_zero_blocks) {
+            pthread_cond_wait(&p->cv, &p->mu);
+            continue;
+        }
         if (!timeout_ms || pthread_cond_timedwait(&p->cv, &p->mu, &dl) != 0) {  /* timeout 0: a poll */
             pthread_mutex_unlock(&p->mu);
             return 0;
@@ -411,7 +425,7 @@ static void *g_lib;
 typedef struct {
     uint32_t max_frames;
     size_t max_bytes;
-    int tx, rx, coalesce_send;
+    int tx, rx, coalesce_send, recv_polls;
 } hb_opts_t;
 typedef struct {
     uint64_t tx_frames, tx_batched_frames, tx_batches, tx_max_batch, rx_frames, rx_batches, rx_max_batch,
@@ -434,7 +448,11 @@ static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
 {
     fn_battach_t at = (fn_battach_t)dlsym(g_lib, "val_batch_attach");
     if (!at) return -1;
-    hb_opts_t o = {0, 0, g_batch_tx, g_batch_rx, g_coalesce};
+    /* this harness's recv polls (timeout 0 returns at once) unless told to
+       behave like the reference's TCP example (VAL_HARNESS_ZERO_BLOCKS) or
+       not to say so (VAL_HARNESS_NO_POLLS) */
+    hb_opts_t o = {0, 0, g_batch_tx, g_batch_rx, g_coalesce, !g_zero_blocks && !getenv("VAL_HARNESS_NO_POLLS")};
+    if (getenv("VAL_HARNESS_FORCE_POLLS")) o.recv_polls = 1;  /* claim polls even if recv blocks (demonstration) */
     if (getenv("VAL_HARNESS_BATCH_FRAMES")) o.max_frames = (uint32_t)atoi(getenv("VAL_HARNESS_BATCH_FRAMES"));
     const char *only = getenv("VAL_HARNESS_BATCH_END");  /* sender|receiver: attach one end only */
     if ((!only || strcmp(only, "receiver")) && at(a, &o, ba) != 0) return -1;
@@ -1378,6 +1396,7 @@ int main(int argc, char **argv)
     g_partial_random = pe && pe[0] == 'r';
     g_seed = getenv("VAL_HARNESS_SEED") ? strtoull(getenv("VAL_HARNESS_SEED"), NULL, 0) : 0u;
     g_partial = pe ? (size_t)strtoul(pe + g_partial_random, NULL, 0) : 0;
+    g_zero_blocks = getenv("VAL_HARNESS_ZERO_BLOCKS") && atoi(getenv("VAL_HARNESS_ZERO_BLOCKS"));
     const char *ce = getenv("VAL_HARNESS_COALESCE");
     g_coalesce = ce ? atoi(ce) : 0;
     const char *be = getenv("VAL_HARNESS_BATCH");

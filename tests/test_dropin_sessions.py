@@ -317,6 +317,36 @@ def test_auto_mode_batches_only_when_a_batch_can_reach_the_gpu(gpu):
 
 @needs_harness
 @pytest.mark.parametrize("gpu", MODES)
+def test_blocking_zero_timeout_transport_does_not_deadlock(gpu):
+    """The reference's own TCP transport treats recv timeout 0 as "wait until
+    the bytes are there" (examples/tcp/common/tcp_util.c:383, select with no
+    timeout); the reference never passes 0 (src/val_core.c:31). A read-ahead
+    that polled such a transport would block at the end of every window
+    until the peer sent more, which it does only after the ACKs: a deadlock
+    (the harness's VAL_HARNESS_FORCE_POLLS shows it hang). With recv_polls = 0,
+    the attach default, the batcher never polls: TX still batches every
+    window, RX reads only what the session asks, and transfers at windows 1,
+    8 and 64 end clean, the window-1 wire equal to the reference's."""
+    with open(os.path.join(ROOT, "tests", "golden", "dropin_vectors.json")) as f:
+        f6 = json.load(f)["loopback"]
+    os.environ["VAL_HARNESS_ZERO_BLOCKS"] = "1"
+    try:
+        for window, mtu in ((0, 1024), (8, 1024), (64, 16404)):
+            got = _line(_run([vc.LIB_PATH, "loopback-batched", 1 << 20, mtu, window], gpu, timeout=120))
+            assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, (window, got)
+            assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"], window
+            tx, rx = got["batch"]
+            assert tx["tx_batches"] > 0 and rx["rx_batches"] == 0 and tx["rx_batches"] == 0, (window, got["batch"])
+            assert rx["direct_answers"] == got["tx_frames"] + got["rx_frames"], window  # every check, per frame
+            if window == 0:
+                assert got["tx_digest"] == f6["tx_digest"] and got["rx_digest"] == f6["rx_digest"]
+            _lib_counters_clean(got, gpu)
+    finally:
+        os.environ.pop("VAL_HARNESS_ZERO_BLOCKS", None)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
 def test_coalesced_window_sends(gpu):
     """coalesce_send (include/val_batch.h): each window goes to the
     application's transport as ONE send of its frames back to back. The

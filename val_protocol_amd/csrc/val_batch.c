@@ -251,9 +251,9 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     const size_t cap = b->opt.max_bytes;
     if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
     const uint32_t t0 = b->ticks ? b->ticks() : 0u;
-    /* not batching now: the frame the session asked for only, its check left
-       to the provider */
-    const int eng = vb_engaged(b, b->opt.rx);
+    /* not batching now (or the transport cannot poll): the frame the session
+       asked for only, its check left to the provider */
+    const int eng = b->opt.recv_polls && vb_engaged(b, b->opt.rx);
     const uint32_t lim = eng ? b->opt.max_frames : 1u;
     uint32_t nread = 0;
     /* a frame carried over from the previous ring is delivered, not batched */
@@ -261,6 +261,9 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     uint64_t fstart = 0;
     int first = 1;
     for (;;) {
+        /* past the first frame every read is a zero-timeout poll: only on a
+           transport that says it polls (val_batch_opts_t.recv_polls) */
+        if (!first && !b->opt.recv_polls) break;
         uint32_t budget = 0;  /* frames read ahead: only what is there */
         if (first) {
             const uint32_t el = b->ticks ? b->ticks() - t0 : 0u;
