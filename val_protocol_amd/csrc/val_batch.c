@@ -259,7 +259,7 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     /* a frame carried over from the previous ring is delivered, not batched */
     int whole = b->hdr_have == 0 && b->owe == 0;
     uint64_t fstart = 0;
-    int first = 1;
+    int first = 1, attempted = 0;
     for (;;) {
         /* past the first frame every read is a zero-timeout poll: only on a
            transport that says it polls (val_batch_opts_t.recv_polls) */
@@ -267,7 +267,11 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
         uint32_t budget = 0;  /* frames read ahead: only what is there */
         if (first) {
             const uint32_t el = b->ticks ? b->ticks() - t0 : 0u;
-            budget = timeout_ms > el ? timeout_ms - el : 0u;
+            if (attempted && el >= timeout_ms) break;  /* the session's time is up: it gets what there is */
+            /* as val_recv_full (src/val_core.c:29-31): never 0 once the
+               session gave a timeout, since a transport may block on 0 */
+            budget = timeout_ms > el ? timeout_ms - el : (timeout_ms ? 1u : 0u);
+            attempted = 1;
         }
         if (b->owe == 0) {  /* the header */
             if (b->hdr_have == 0) {
