@@ -454,6 +454,7 @@ static int batch_attach(val_config_t *a, val_config_t *b, void **ba, void **bb)
     hb_opts_t o = {0, 0, g_batch_tx, g_batch_rx, g_coalesce, !g_zero_blocks && !getenv("VAL_HARNESS_NO_POLLS")};
     if (getenv("VAL_HARNESS_FORCE_POLLS")) o.recv_polls = 1;  /* claim polls even if recv blocks (demonstration) */
     if (getenv("VAL_HARNESS_BATCH_FRAMES")) o.max_frames = (uint32_t)atoi(getenv("VAL_HARNESS_BATCH_FRAMES"));
+    if (getenv("VAL_HARNESS_BATCH_BYTES")) o.max_bytes = (size_t)strtoull(getenv("VAL_HARNESS_BATCH_BYTES"), NULL, 0);
     const char *only = getenv("VAL_HARNESS_BATCH_END");  /* sender|receiver: attach one end only */
     if ((!only || strcmp(only, "receiver")) && at(a, &o, ba) != 0) return -1;
     if ((!only || strcmp(only, "sender")) && at(b, &o, bb) != 0) return -1;

@@ -347,6 +347,33 @@ def test_blocking_zero_timeout_transport_does_not_deadlock(gpu):
 
 @needs_harness
 @pytest.mark.parametrize("gpu", MODES)
+@pytest.mark.parametrize("frames,nbytes", [(1, 0), (3, 0), (0, 9000), (5, 20000)], ids=["f1", "f3", "b9000", "f5b20000"])
+def test_batch_limits_below_the_window(gpu, frames, nbytes):
+    """max_frames / max_bytes below the window (64 frames of MTU 4,096): the
+    window is hashed and sent in several batches, read-ahead stops at the
+    limits (max_bytes is raised to one MTU at least), and the transfer is
+    unchanged: clean, equal, every trailer the reference's, every receiver
+    check answered from a batch."""
+    env = {"VAL_HARNESS_BATCH_FRAMES": str(frames), "VAL_HARNESS_BATCH_BYTES": str(nbytes)}
+    os.environ.update(env)
+    try:
+        got = _line(_run([vc.LIB_PATH, "loopback-batched", 3_000_000, 4096, 64], gpu))
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+    assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"]
+    tx, rx = got["batch"]
+    cap = frames or 65535
+    if nbytes:
+        cap = min(cap, max(nbytes, 4096) // 1000)  # frames of at most 4,096 wire bytes, at least ~1,000
+    assert 1 <= tx["tx_max_batch"] <= max(cap, 1) and 1 <= rx["rx_max_batch"] <= max(cap, 1), (cap, got["batch"])
+    assert rx["rx_batched_answers"] >= 3_000_000 // (4096 - 12)
+    _lib_counters_clean(got, gpu)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
 def test_coalesced_window_sends(gpu):
     """coalesce_send (include/val_batch.h): each window goes to the
     application's transport as ONE send of its frames back to back. The
