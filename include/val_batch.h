@@ -45,7 +45,8 @@
  * window fill, the receiver reads ahead). Measured on the reference's own
  * loopback, that moved the transfer rate by -24% to +14% against the plain
  * provider depending on window and direction. So in
- * AUTO a direction batches only when its largest possible batch,
+ * AUTO a direction batches only when a device was present at attach and
+ * its largest possible batch,
  * min(max_bytes, window_cap_packets x packet_size), reaches the crossover
  * (checked at every window, so val_gpu_set_host_batch_min_bytes takes effect
  * at once); otherwise TX frames get their trailer from the provider and go
@@ -61,6 +62,10 @@
  * its recv polls (recv_polls = 1). Such a poll must also be cheap: a
  * condition-variable wait on an already expired deadline took ~70 us per
  * empty poll in our harness and added that to every read-ahead.
+ *
+ * A batch the GPU path fails is computed on the CPU engine instead
+ * (batch_fallbacks): like the provider, the batcher never fails a session
+ * over a device error.
  *
  * The application keeps its own transport and provider semantics: the
  * wrapped hooks call the ones in the config at attach time (a NULL provider
@@ -87,7 +92,8 @@ extern "C" {
 
 typedef struct {
     uint32_t max_frames;  /* frames per batch, TX and RX (0 = 65,535) */
-    size_t max_bytes;     /* wire bytes per batch (0 = 16 MiB; at least one MTU) */
+    size_t max_bytes;     /* wire bytes per batch (0 = window_cap_packets x packet_size within [16, 256] MiB;
+                             at least one MTU) */
     int tx;               /* VAL_BATCH_*: defer TX trailers to window batches */
     int rx;               /* VAL_BATCH_*: read ahead and hash RX frames in batches */
     int coalesce_send;    /* 1: one transport.send per flushed window (0: one per frame, as the reference) */
@@ -107,6 +113,7 @@ typedef struct {
     uint64_t rx_max_batch;       /* most frames in one RX batch */
     uint64_t rx_batched_answers; /* provider calls answered from an RX batch */
     uint64_t direct_answers;     /* provider calls computed directly (resume windows, split frames) */
+    uint64_t batch_fallbacks;    /* batches the GPU path failed and the CPU engine computed (the provider's policy) */
     int32_t status;              /* first transport or batch failure (VAL_OK if none) */
 } val_batch_stats_t;
 

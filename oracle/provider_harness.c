@@ -429,7 +429,7 @@ typedef struct {
 } hb_opts_t;
 typedef struct {
     uint64_t tx_frames, tx_batched_frames, tx_batches, tx_max_batch, rx_frames, rx_batches, rx_max_batch,
-        rx_batched_answers, direct_answers;
+        rx_batched_answers, direct_answers, batch_fallbacks;
     int32_t status;
 } hb_stats_t;
 typedef int (*fn_battach_t)(val_config_t *, const hb_opts_t *, void **);
@@ -473,12 +473,13 @@ static void batch_report(FILE *out, void *ba, void *bb)
     for (int k = 0; k < 2; k++)
         fprintf(out, "%s{\"end\":\"%s\",\"tx_frames\":%llu,\"tx_batched_frames\":%llu,\"tx_batches\":%llu,\"tx_max_batch\":%llu,"
                "\"rx_frames\":%llu,\"rx_batches\":%llu,\"rx_max_batch\":%llu,\"rx_batched_answers\":%llu,"
-               "\"direct_answers\":%llu,\"status\":%d}",
+               "\"direct_answers\":%llu,\"batch_fallbacks\":%llu,\"status\":%d}",
                k ? "," : "", k ? "receiver" : "sender", (unsigned long long)st[k].tx_frames,
                (unsigned long long)st[k].tx_batched_frames, (unsigned long long)st[k].tx_batches,
                (unsigned long long)st[k].tx_max_batch, (unsigned long long)st[k].rx_frames,
                (unsigned long long)st[k].rx_batches, (unsigned long long)st[k].rx_max_batch,
-               (unsigned long long)st[k].rx_batched_answers, (unsigned long long)st[k].direct_answers, st[k].status);
+               (unsigned long long)st[k].rx_batched_answers, (unsigned long long)st[k].direct_answers,
+               (unsigned long long)st[k].batch_fallbacks, st[k].status);
     fprintf(out, "]");
     dt(ba);
     dt(bb);

@@ -373,6 +373,32 @@ def test_batch_limits_below_the_window(gpu, frames, nbytes):
 
 
 @needs_harness
+def test_failed_gpu_batches_fall_back_to_the_cpu_engine():
+    """The provider has no error channel, so neither may the
+    batcher fail a session over a batch the GPU path cannot take: here every
+    batch is sent to the GPU path (threshold 0) in a container without a GPU,
+    each fails with VAL_ERR_IO, and the batcher computes those CRCs on the
+    CPU engine instead (counted in batch_fallbacks). The transfer ends clean
+    with every trailer the reference's."""
+    vc.lib()
+    env = dict(os.environ, VAL_GPU_HOST_BATCH_MIN_BYTES="0")
+    env.pop("VAL_GPU_PROVIDER_MIN_BYTES", None)
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("needs a host without a GPU")
+    r = subprocess.run([HARNESS, vc.LIB_PATH, "loopback-batched", str(1 << 20), "1024", "8"], capture_output=True,
+                       text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = _line(r.stdout)
+    assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+    assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"]
+    tx, rx = got["batch"]
+    assert tx["status"] == VAL_OK and rx["status"] == VAL_OK
+    assert tx["batch_fallbacks"] >= tx["tx_batches"] > 0 and rx["batch_fallbacks"] == rx["rx_batches"] > 0, got["batch"]
+
+
+@needs_harness
 @pytest.mark.parametrize("gpu", MODES)
 def test_coalesced_window_sends(gpu):
     """coalesce_send (include/val_batch.h): each window goes to the

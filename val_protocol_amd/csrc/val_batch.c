@@ -16,7 +16,8 @@
 #include "val_wire.h"
 
 #define VB_MAX_ATTACHED 256
-#define VB_DEFAULT_BYTES ((size_t)16u << 20)
+#define VB_MIN_DEFAULT_BYTES ((size_t)16u << 20)   /* default max_bytes: the window, within these */
+#define VB_MAX_DEFAULT_BYTES ((size_t)256u << 20)
 #define VB_DEFAULT_FRAMES 65535u
 
 typedef struct {
@@ -49,6 +50,7 @@ struct val_batch {
     size_t tx_pending;  /* CRC input of the frame whose placeholder was just returned (0: none) */
     /* RX ring: bytes [r_head, r_len) not yet handed to the session */
     uint8_t *rx;
+    size_t rx_cap;  /* the ring's bytes: max_bytes with read-ahead, else one frame */
     size_t r_head, r_len;
     vb_frame_t *rxf;
     uint32_t rx_n, rx_cur;  /* complete frames in the ring; the one being delivered */
@@ -105,6 +107,7 @@ static int vb_engaged(const val_batch_t *b, int mode)
 {
     if (mode == VAL_BATCH_ALWAYS) return 1;
     if (mode != VAL_BATCH_AUTO) return 0;
+    if (!b->pinned) return 0;  /* no device at attach: every batch would run on the CPU engine */
     uint64_t ub = (uint64_t)b->win_cap * b->mtu;
     if (ub > b->opt.max_bytes) ub = b->opt.max_bytes;
     return ub >= val_gpu_host_batch_min_bytes();
@@ -126,8 +129,15 @@ static val_status_t vb_hash(val_batch_t *b, const uint8_t *buf, size_t used, vb_
             k++;
         }
     if (!k) return VAL_OK;
-    val_status_t st = val_crc32_frames_host(buf, used, b->off_tmp, b->len_tmp, 0, 0, k, b->crc_tmp, NULL);
-    if (st != VAL_OK) return st;
+    const val_status_t st = val_crc32_frames_host(buf, used, b->off_tmp, b->len_tmp, 0, 0, k, b->crc_tmp, NULL);
+    if (st == VAL_ERR_INVALID_ARG) return st;  /* our own descriptors: a bug, not a device failure */
+    if (st != VAL_OK) {
+        /* the provider's failure policy (it has no error channel):
+           a batch the GPU could not take is computed on the CPU engine */
+        for (uint32_t i = 0; i < k; i++)
+            b->crc_tmp[i] = val_crc32_cpu_update_state(0xFFFFFFFFu, buf + b->off_tmp[i], b->len_tmp[i], 0) ^ 0xFFFFFFFFu;
+        b->st.batch_fallbacks++;
+    }
     k = 0;
     for (uint32_t i = 0; i < n; i++)
         if (!only_needed || f[i].need) f[i].crc = b->crc_tmp[k++];
@@ -248,7 +258,7 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
     b->r_base += b->r_len;
     b->r_head = b->r_len = 0;
     b->rx_n = b->rx_cur = 0;
-    const size_t cap = b->opt.max_bytes;
+    const size_t cap = b->rx_cap;
     if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
     const uint32_t t0 = b->ticks ? b->ticks() : 0u;
     /* not batching now (or the transport cannot poll): the frame the session
@@ -471,10 +481,18 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
         return VAL_ERR_INVALID_ARG;
     }
     if (!b->opt.max_frames) b->opt.max_frames = VB_DEFAULT_FRAMES;
-    if (!b->opt.max_bytes) b->opt.max_bytes = VB_DEFAULT_BYTES;
     b->mtu = cfg->buffers.packet_size;
     b->win_cap = cfg->tx_flow.window_cap_packets ? cfg->tx_flow.window_cap_packets : 1u;
+    if (!b->opt.max_bytes) {  /* the window's bytes, within [16, 256] MiB: a window that can reach the GPU fits */
+        const uint64_t w = (uint64_t)b->win_cap * b->mtu;
+        b->opt.max_bytes = w < VB_MIN_DEFAULT_BYTES ? VB_MIN_DEFAULT_BYTES
+                                                    : w > VB_MAX_DEFAULT_BYTES ? VB_MAX_DEFAULT_BYTES : (size_t)w;
+    }
     if (b->opt.max_bytes < b->mtu) b->opt.max_bytes = b->mtu;
+    /* buffers only where they can be used: no TX window without TX batching,
+       an RX ring of one frame without read-ahead */
+    const size_t tx_cap = b->opt.tx ? b->opt.max_bytes : 16u;
+    b->rx_cap = (b->opt.rx && b->opt.recv_polls) ? b->opt.max_bytes : b->mtu;
     b->cfg = cfg;
     b->u_send = cfg->transport.send;
     b->u_recv = cfg->transport.recv;
@@ -487,8 +505,8 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     b->recv_buffer = (const uint8_t *)cfg->buffers.recv_buffer;
     b->pinned = val_gpu_device_count() > 0;  /* pinned windows: DMA in place on the GPU path */
     const uint32_t nf = b->opt.max_frames;
-    b->tx = (uint8_t *)vb_alloc(b, b->opt.max_bytes, &b->tx_pinned);
-    b->rx = (uint8_t *)vb_alloc(b, b->opt.max_bytes, &b->rx_pinned);
+    b->tx = (uint8_t *)vb_alloc(b, tx_cap, &b->tx_pinned);
+    b->rx = (uint8_t *)vb_alloc(b, b->rx_cap, &b->rx_pinned);
     b->txf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
     b->rxf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
     b->crc_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
