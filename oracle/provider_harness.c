@@ -787,8 +787,11 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     fclose(f);
 
     pipe_t a2b, b2a;
-    pipe_init(&a2b, 64u << 20);
-    pipe_init(&b2a, 64u << 20);
+    /* room for two full windows in flight (64 MiB at least) */
+    const size_t pwin = (size_t)2u * (window ? window : 1u) * mtu + ((size_t)1u << 20);
+    const size_t pcap = pwin > ((size_t)64u << 20) ? pwin : ((size_t)64u << 20);
+    pipe_init(&a2b, pcap);
+    pipe_init(&b2a, pcap);
     end_t etx = {&a2b, &b2a, 0xFFFFFFFFu, 0, NULL, 0, 0, 0}, erx = {&b2a, &a2b, 0xFFFFFFFFu, 0, NULL, 0, 0, 0};
     etx.caplog = erx.caplog = 4096;
     etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
