@@ -249,10 +249,11 @@ static size_t vb_content_max(const val_batch_t *b)
 
 /* Refill the empty ring: the frame in progress (or the next one), for which
  * the transport is given up to timeout_ms as the session would give it (over
- * as many partial reads as it takes), then every further byte the transport
- * already holds (zero-timeout polls, until one returns nothing). Complete
- * frames that began in this ring are hashed in one batch. Returns 0, or -1 on
- * a transport error. */
+ * as many partial reads as it takes), then, on a transport that polls
+ * (recv_polls), every further byte it already holds (zero-timeout polls,
+ * until one returns nothing). Complete frames that began in this ring are
+ * hashed in one batch when this direction batches. Returns 0, or -1 on a
+ * transport error. */
 static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
 {
     b->r_base += b->r_len;
