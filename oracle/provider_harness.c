@@ -211,6 +211,7 @@ typedef struct {
     unsigned long recvs;  /* transport.recv calls of this end: frames sent between two are one window fill */
     unsigned long flip_every, data_sent, flipped;  /* fault injection: one payload bit of every Nth DATA frame */
     uint64_t rng;  /* partial-read sizes (VAL_HARNESS_PARTIAL=rN) */
+    unsigned long drop_every, data_sent_d, dropped;  /* fault injection: every Nth DATA frame lost */
 } end_t;
 
 /* VAL_HARNESS_FLIP_EVERY=N: the sender's pipe flips one payload bit of every
@@ -220,6 +221,16 @@ typedef struct {
 static unsigned long flip_every_env(void)
 {
     const char *e = getenv("VAL_HARNESS_FLIP_EVERY");
+    return e ? strtoul(e, NULL, 0) : 0ul;
+}
+
+/* VAL_HARNESS_DROP_EVERY=N: the sender's pipe loses every Nth DATA frame it
+ * carries (after logging it), as the reference's net simulator drops packets
+ * (unit_tests/support/test_support.c): the receiver must miss it, the
+ * sender retransmit, and the transfer still complete. */
+static unsigned long drop_every_env(void)
+{
+    const char *e = getenv("VAL_HARNESS_DROP_EVERY");
     return e ? strtoul(e, NULL, 0) : 0ul;
 }
 
@@ -238,6 +249,11 @@ static int tp_send(void *ctx, const void *data, size_t len)
         memcpy(r->bytes, data, len);
         r->len = len;
         r->epoch = e->recvs;
+    }
+    if (e->drop_every && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA &&
+        ++e->data_sent_d % e->drop_every == 0) {
+        e->dropped++;
+        return (int)len;  /* "sent": lost on the way */
     }
     if (e->flip_every && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA &&
         ++e->data_sent % e->flip_every == 0) {
@@ -797,6 +813,7 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     etx.log = (frame_rec_t *)malloc(etx.caplog * sizeof(frame_rec_t));
     erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
     etx.flip_every = flip_every_env();
+    etx.drop_every = drop_every_env();
     etx.rng = g_seed * 2u + 1u;  /* partial-read draws (VAL_HARNESS_PARTIAL=rN), per end */
     erx.rng = g_seed * 2u + 2u;
     crc32_func_t prov = use_gpu ? counting_provider : NULL;
@@ -840,11 +857,11 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     fprintf(out_json, "{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
            "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
-           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"wire_frames\":%lu,\"flipped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"wire_frames\":%lu,\"flipped\":%lu,\"dropped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
            "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
            use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
            mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
-           t_ok, wf_tx + wf_rx, etx.flipped, __atomic_load_n(&g_calls, __ATOMIC_RELAXED), t1 - t0,
+           t_ok, wf_tx + wf_rx, etx.flipped, etx.dropped, __atomic_load_n(&g_calls, __ATOMIC_RELAXED), t1 - t0,
            (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
            (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
            (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));

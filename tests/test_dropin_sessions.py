@@ -189,6 +189,28 @@ def test_corrupted_frames_detected_like_the_reference(gpu):
 
 @needs_harness
 @pytest.mark.parametrize("gpu", MODES)
+def test_dropped_frames_recovered_like_the_reference(gpu):
+    """Frame loss (the sender's pipe drops every 200th DATA frame, as the
+    reference's net simulator drops packets): at windows 1 and 8 the plain and
+    the batched product recover exactly as the reference's built-in-CRC run
+    does: same timeouts, retransmissions and wire digests, the file equal."""
+    os.environ["VAL_HARNESS_DROP_EVERY"] = "200"
+    try:
+        for window in (0, 8):
+            ref = _line(_run(["none", "loopback", 1 << 20, 1024, window], gpu))
+            assert ref["dropped"] >= 5 and ref["equal"] == 1 and ref["retransmits"] >= ref["dropped"], ref
+            for mode in ("loopback", "loopback-batched"):
+                got = _line(_run([vc.LIB_PATH, mode, 1 << 20, 1024, window], gpu))
+                for k in ("tx_status", "rx_status", "equal", "dropped", "retransmits", "timeouts", "tx_digest",
+                          "rx_digest"):
+                    assert got[k] == ref[k], (window, mode, k, got[k], ref[k])
+                _lib_counters_clean(got, gpu)
+    finally:
+        os.environ.pop("VAL_HARNESS_DROP_EVERY", None)
+
+
+@needs_harness
+@pytest.mark.parametrize("gpu", MODES)
 def test_parallel_batched_sessions(gpu):
     """Four batched transfers at once (eight session threads; reference
     include/val_protocol.h:231-233: sessions run in parallel): every
