@@ -137,3 +137,55 @@ def test_batch_attach_argument_checks():
         out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
     assert [int(v) for v in out] == [vc.VAL_ERR_INVALID_ARG, 0, 1, vc.VAL_ERR_INVALID_ARG, 1, 0,
                                      vc.VAL_ERR_INVALID_ARG, 0, 12]
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_batch_registry_capacity_and_reuse():
+    """Up to 256 attached configs per process (include/val_batch.h): the 257th
+    attach is refused, detaching frees the slots for reuse, and the provider
+    on a buffer of no attached config answers with the plain CRC."""
+    src = r"""
+    #include "val_batch.h"
+    #include <stdio.h>
+    #include <string.h>
+    #include <stdlib.h>
+    static int snd(void *c, const void *d, size_t n) { (void)c; (void)d; return (int)n; }
+    static int rcv(void *c, void *b, size_t n, size_t *g, uint32_t t) { (void)c; (void)b; (void)n; (void)t; *g = 0; return 0; }
+    int main(void) {
+        static val_config_t cfg[257];
+        static char buf[257][2][64];
+        val_batch_t *b[257];
+        val_batch_opts_t o;
+        memset(&o, 0, sizeof o);
+        o.max_frames = 4;
+        o.max_bytes = 64;
+        int ok = 0;
+        for (int i = 0; i < 257; i++) {
+            memset(&cfg[i], 0, sizeof cfg[i]);
+            cfg[i].transport.send = snd;
+            cfg[i].transport.recv = rcv;
+            cfg[i].buffers.packet_size = 64;
+            cfg[i].buffers.send_buffer = buf[i][0];
+            cfg[i].buffers.recv_buffer = buf[i][1];
+            b[i] = NULL;
+            ok += val_batch_attach(&cfg[i], &o, &b[i]) == 0;
+        }
+        const char kat[] = "123456789";
+        unsigned plain = val_batch_crc32_provider(0xFFFFFFFFu, kat, 9);
+        for (int i = 0; i < 256; i++) val_batch_detach(b[i]);
+        int again = val_batch_attach(&cfg[256], &o, &b[256]) == 0;
+        val_batch_detach(b[256]);
+        printf("%d %d %08x\n", ok, again, plain);
+        return 0;
+    }
+    """
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        libdir = os.path.dirname(vc.LIB_PATH)
+        vc.lib()
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", f"-I{INC}", c, "-o", exe, f"-L{libdir}",
+                        "-l:libval_crc_hip.so", f"-Wl,-rpath,{libdir}"], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    assert out == ["256", "1", "cbf43926"]
