@@ -1048,7 +1048,29 @@ val_status_t region_host(const void *data, size_t len, uint32_t state_in, uint32
 // val_gpu_set_cpu_fallback(0) makes a failed hook abort instead. Nothing else
 // has a CPU path: batch calls return VAL_ERR_IO.
 std::atomic<uint64_t> g_cpu_fallbacks{0};
-std::atomic<uint64_t> g_cpu_small{0};
+// Hook calls answered below the provider threshold: counted on every VAL frame
+// by every session thread, so the count is sharded over cache lines (one per
+// thread, round-robin) and summed on read. One shared counter made concurrent
+// sessions take turns on its line: 16-B calls cost 24 ns on one thread and
+// 373 ns each on eight (the provider's whole cost, oracle/provider_bench.c).
+struct alignas(64) CountShard {
+    std::atomic<uint64_t> v{0};
+};
+constexpr int kCountShards = 64;
+CountShard g_cpu_small[kCountShards];
+std::atomic<uint32_t> g_next_shard{0};
+thread_local int t_count_shard = -1;
+inline void count_small()
+{
+    if (t_count_shard < 0) t_count_shard = (int)(g_next_shard.fetch_add(1, std::memory_order_relaxed) % kCountShards);
+    g_cpu_small[t_count_shard].v.fetch_add(1, std::memory_order_relaxed);
+}
+uint64_t cpu_small_total()
+{
+    uint64_t t = 0;
+    for (const CountShard &c : g_cpu_small) t += c.v.load(std::memory_order_relaxed);
+    return t;
+}
 std::atomic<int> g_cpu_fallback_on{-1};  // -1: from the environment
 std::atomic<int64_t> g_provider_min{-1};  // -1: from the environment, else the default
 thread_local int t_hook_path = VAL_GPU_HOOK_NONE;
@@ -1085,7 +1107,7 @@ uint32_t scalar_state(const char *fn, uint32_t state, const void *data, size_t l
     if (len && !data) die(fn);  // the reference dereferences it too
     if ((uint64_t)len < provider_min_bytes()) {
         t_hook_path = VAL_GPU_HOOK_CPU;
-        g_cpu_small.fetch_add(1, std::memory_order_relaxed);
+        count_small();
         return vcrc_cpu_update(state, data, len);
     }
     if (region_host(data, len, state, &out) == VAL_OK) {
@@ -1861,7 +1883,7 @@ uint32_t val_gpu_scratch_entries(int device, uint64_t *evictions)
     return (uint32_t)c->scratch.size();
 }
 
-uint64_t val_gpu_cpu_small_count(void) { return g_cpu_small.load(std::memory_order_relaxed); }
+uint64_t val_gpu_cpu_small_count(void) { return cpu_small_total(); }
 
 int val_gpu_last_hook_path(void) { return t_hook_path; }
 
