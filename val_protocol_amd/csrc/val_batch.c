@@ -81,12 +81,41 @@ static val_batch_t *g_reg[VB_MAX_ATTACHED];
 static const void *g_buf[2][VB_MAX_ATTACHED];  /* [0]: send_buffer, [1]: recv_buffer */
 static int g_hwm;  /* slots [0, g_hwm) have been used: the provider scans only those */
 
-static val_batch_t *vb_lookup(const void *buf, int rx)
+/* The slot this thread last found per direction: a session's thread calls the
+ * provider on the same two buffers frame after frame, so the scan (up to 256
+ * slots once many sessions are attached) runs once per thread and session.
+ * The hint is only a starting guess: a slot matches only if it holds this very
+ * buffer now. */
+static __thread int t_slot_hint[2] = {-1, -1};
+
+/* The attached batcher whose send_buffer (*rx = 0) or recv_buffer (*rx = 1)
+ * is buf, or NULL. */
+static val_batch_t *vb_find(const void *buf, int *rx)
 {
+    if (!buf) return NULL;  /* a free slot's buffers read NULL */
+    for (int d = 0; d < 2; d++) {
+        const int h = t_slot_hint[d];
+        if (h >= 0 && __atomic_load_n(&g_buf[d][h], __ATOMIC_ACQUIRE) == buf) {
+            *rx = d;
+            return __atomic_load_n(&g_reg[h], __ATOMIC_ACQUIRE);
+        }
+    }
     const int hwm = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
     for (int i = 0; i < hwm; i++)
-        if (__atomic_load_n(&g_buf[rx][i], __ATOMIC_ACQUIRE) == buf) return __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
+        for (int d = 0; d < 2; d++)
+            if (__atomic_load_n(&g_buf[d][i], __ATOMIC_ACQUIRE) == buf) {
+                t_slot_hint[d] = i;
+                *rx = d;
+                return __atomic_load_n(&g_reg[i], __ATOMIC_ACQUIRE);
+            }
     return NULL;
+}
+
+static val_batch_t *vb_lookup(const void *buf, int rx)
+{
+    int d = 0;
+    val_batch_t *b = vb_find(buf, &d);
+    return d == rx ? b : NULL;
 }
 
 static uint32_t vb_direct(val_batch_t *b, uint32_t seed, const void *buf, size_t len)
@@ -413,8 +442,9 @@ static int vb_recv(void *ctx, void *buffer, size_t size, size_t *received, uint3
 /* ---- the provider ------------------------------------------------------ */
 uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
 {
-    val_batch_t *b = vb_lookup(buf, 0);
-    if (b) {
+    int rx = 0;
+    val_batch_t *b = vb_find(buf, &rx);
+    if (b && !rx) {
         /* a DATA frame (its type byte leads the header, src/val_core.c:828-835)
            while batching: the trailer comes later from the window batch;
            control frames (ACK, DONE, ...) go out alone at once, so they are
@@ -426,7 +456,6 @@ uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
         }
         return vb_direct(b, seed, buf, len);
     }
-    b = vb_lookup(buf, 1);
     if (b && b->armed && seed == 0xFFFFFFFFu && len == b->armed_len) {
         b->armed = 0;
         b->st.rx_batched_answers++;
