@@ -56,6 +56,15 @@ def parse():
     ap.add_argument("--with-cfg4-strong", action="store_true",
                     help="also time the cfg4 strong-scaling block after a weak config other than cfg3 "
                          "(by default only the cfg3 headline line carries it)")
+    ap.add_argument("--no-cfg4-proxy", action="store_true",
+                    help="N=1: skip the single-GPU proxy of cfg4's 2/4/8-GPU slices after the cfg4 block")
+    ap.add_argument("--cfg4-alloc-first", action="store_true",
+                    help="allocate the cfg4 block's buffer before the headline's (placement A/B)")
+    ap.add_argument("--block-warmup-ms", type=float, default=100.0,
+                    help="cfg4 block: after its --warmup launches, further untimed launches up to this much GPU "
+                         "time (the block follows ~20 s of host-side work with the GPU idle; with 5 launches of "
+                         "warm-up it ran 1%% slower than cfg4 alone, with 100 ms 0.5%% faster: "
+                         "profiles/r06_ab_cfg4_block.jsonl)")
     return ap.parse_args()
 
 
@@ -499,12 +508,144 @@ def verify_windows(torch, vc, flat, dev, stream):
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_command(n: int, argv: list, port: int) -> list:
+    """The one-process-per-GPU command `bench.py --gpus N` starts for N > 1
+    when it was not launched under torch.distributed.run: the same script and
+    arguments under torchrun, N ranks on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n: int, backend: str) -> int:
+    """`bench.py --gpus N` (N > 1) run as a plain process: start the N ranks
+    as a fresh child process (torch.distributed.run), wait for it and return
+    its exit status. Decided before this process touches the GPU (the device
+    count below does not initialise it) and never by exec: the ranks are a
+    child, their JSON line reaches the caller on the inherited stdout."""
+    import signal
+    import subprocess
+
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs for the nccl (RCCL) backend, found {ndev}; one rank "
+              f"per GPU (VAL_BENCH_BACKEND=gloo rehearses several ranks on one GPU)", file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ, VAL_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child)")
+    cmd = rank_launch_command(n, sys.argv[1:], _free_port())
+    print(f"[bench] starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    child = subprocess.Popen(cmd, env=env)
+
+    def forward(sig, _frame):  # a timeout's SIGTERM to this process ends the ranks too
+        child.send_signal(sig)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    return child.wait()
+
+
+def block_warmup(torch, step, steps, min_ms, stream):
+    """Untimed launches before an extra block: `steps` of them, then more
+    until at least `min_ms` of GPU time has run (the block follows minutes of
+    host-side work with the GPU idle, and its clocks settle over ~30 ms of
+    load). Returns the number of launches run."""
+    done = 0
+    for _ in range(steps):
+        step()
+        done += 1
+    if min_ms <= 0:
+        torch.cuda.synchronize()
+        return done
+    spent = 0.0
+    while spent < min_ms:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(4):
+            step()
+        b.record(stream)
+        torch.cuda.synchronize()
+        spent += a.elapsed_time(b)
+        done += 4
+    return done
+
+
+def roofline_block(nbytes, kern_ms, roof):
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4), "bytes_per_launch": nbytes,
+            "read_roof": round(roof, 1) if roof else None,
+            "frac_of_read_roof": round(achieved / roof, 4) if roof else None,
+            "read_roof_frac_of_peak": round(roof / HBM_PEAK_GBS, 4) if roof else None}
+
+
+def cfg4_strong_proxy(torch, dist, vc, w4, stream, steps, warmup, block_kern_ms):
+    """Single-GPU proxy of cfg4's 1/2/4/8-GPU strong-scaling curve (north_star:
+    "absolute GiB/s at 1/2/4/8 GPUs"; no multi-GPU node is available to this
+    run). For each N the file is split exactly as N ranks split it
+    (val_shard_frames), and on this one GPU the largest slice and the last
+    rank's slice (it holds the 800-B tail frame) are each timed alone, like the
+    block: W untimed launches, K back-to-back launches between two events on
+    the launch stream. Each N's estimated aggregate = the file's CRC input /
+    the slower of the two slice times: what N GPUs that each run like this one
+    would reach, without node-level effects (placement, PCIe/xGMI, clocks)."""
+    from val_protocol_amd.shard import shard_frames
+
+    n_total, stride, flen = w4["n_total"], w4["stride"], w4["flen"]
+    job = w4["job_bytes"]
+    out = {"label": "single-GPU proxy; no multi-GPU node: each N's slices timed alone on this one GPU",
+           "file_crc_input_bytes": job, "unit": "GiB/s",
+           "1": {"frames": n_total, "kernel_ms": round(block_kern_ms, 4),
+                 "GiB_s_per_gpu": round(job / (block_kern_ms * 1e-3) / GIB, 2),
+                 "est_aggregate_GiB_s": round(job / (block_kern_ms * 1e-3) / GIB, 2), "source": "cfg4_strong block"}}
+    for nr in (2, 4, 8):
+        shards = [shard_frames(n_total, nr, r) for r in range(nr)]
+        big = max(range(nr), key=lambda r: (shards[r][1], -r))
+        slices = []
+        for r in sorted({big, nr - 1}):
+            first, cnt = shards[r]
+            view = w4["flat"][first * stride:(first + cnt) * stride]
+            ln = w4["d_len"][first:first + cnt]
+            off = w4["d_off"][:cnt]  # uniform stride: a slice's offsets from its own base are the first cnt
+            crc = torch.empty(cnt, dtype=torch.int32, device=view.device)
+            step = lambda: vc.frames(view, off=off, length=ln, n=cnt, len_hint=flen, out_crc=crc)  # noqa: E731
+            _, km = timed_steps(torch, dist, 1, step, steps, warmup, stream)
+            sw = {"n": cnt, "flat": view, "desc": True, "d_off": off, "d_len": ln, "crc": crc}
+            ok = parity_sample(torch, sw, r, False, None)
+            nbytes = int(ln.long().sum().item())
+            slices.append({"rank": r, "frames": cnt, "bytes": nbytes, "kernel_ms": round(km, 4),
+                           "GiB_s_per_gpu": round(nbytes / (km * 1e-3) / GIB, 2), "parity_sample_ok": ok,
+                           "last_frame_crc_input": int(ln[cnt - 1].item())})
+        slow = max(s["kernel_ms"] for s in slices)
+        out[str(nr)] = {"frames": max(s["frames"] for s in slices), "kernel_ms": slow,
+                        "GiB_s_per_gpu": min(s["GiB_s_per_gpu"] for s in slices),
+                        "est_aggregate_GiB_s": round(job / (slow * 1e-3) / GIB, 2),
+                        "slices_timed": slices}
+    out["parity_sample_ok"] = all(s["parity_sample_ok"] for k in ("2", "4", "8") for s in out[k]["slices_timed"])
+    return out
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    backend = os.environ.get("VAL_BENCH_BACKEND", "nccl")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, backend))
+    world = int(env_world or "1")
+    if args.gpus < 1 or world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher started a different number of "
+              f"ranks than the run asks for", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("VAL_BENCH_BACKEND", "nccl")
     import torch
     import torch.distributed as dist
 
@@ -530,6 +671,10 @@ def main():
     import val_protocol_amd.crc as vc
 
     vc.init(gpu)
+    want_strong = (args.config == "cfg3" or args.with_cfg4_strong) and not args.no_cfg4_strong \
+        and args.config != "cfg4" and not args.verify and not args.sort_frames
+    # --cfg4-alloc-first: the cfg4 block's buffer is placed before the headline's (diagnostic A/B)
+    w4 = build_workload(torch, dev, "cfg4", rank, world, False, vc) if want_strong and args.cfg4_alloc_first else None
     w = build_workload(torch, dev, args.config, rank, world, args.verify, vc)
     if w["ragged"] and args.sort_frames:
         perm = torch.argsort(w["d_len"])
@@ -624,26 +769,32 @@ def main():
     # BASELINE configs[3] in the same invocation: one 8 GiB file at MTU
     # 65,536 sharded over the ranks by val_shard_frames (strong scaling),
     # timed like the headline, its own per-rank records and aggregate.
-    strong_block = None
-    want_strong = (args.config == "cfg3" or args.with_cfg4_strong) and not args.no_cfg4_strong
-    if want_strong and not strong and not args.verify and not args.sort_frames:
+    strong_block = proxy = None
+    if want_strong:
         del flats, flat, buf, w, crc, hdr, ok, pay, kw
         torch.cuda.empty_cache()
-        w4 = build_workload(torch, dev, "cfg4", rank, world, False, vc)
+        if w4 is None:
+            w4 = build_workload(torch, dev, "cfg4", rank, world, False, vc)
         step4 = lambda: vc.frames(w4["flat"], out_crc=w4["crc"], **w4["kw"])  # noqa: E731
-        el4, km4 = timed_steps(torch, dist, world, step4, args.steps, args.warmup, stream)
+        warm4 = block_warmup(torch, step4, args.warmup, args.block_warmup_ms, stream)
+        el4, km4 = timed_steps(torch, dist, world, step4, args.steps, 0, stream)
         el4_max = max_over_ranks(torch, dist, world, el4, dev, backend)
         par4 = parity_sample(torch, w4, rank, False, None)
         pr4 = gather(dist, world, rank_record(w4, rank, gpu, args.steps, el4, km4, par4))
         tb4 = w4["job_bytes"] * args.steps
+        roof4 = read_roof(torch, w4["flat"], stream) if rank == 0 else None
+        if rank == 0 and world == 1 and not args.no_cfg4_proxy:
+            proxy = cfg4_strong_proxy(torch, dist, vc, w4, stream, args.steps, args.warmup, km4)
         strong_block = {
             "workload": f"cfg4: one {CFG4_FILE >> 30} GiB file as {w4['n_total']} DATA frames of "
                         f"{CONFIGS['cfg4'][1]} B payload (last frame {CFG4_FILE - (w4['n_total'] - 1) * CONFIGS['cfg4'][1]} B), "
                         f"sharded over {world} GPU{'s' if world > 1 else ''} by contiguous byte-balanced frame ranges "
                         f"(val_shard_frames, no collective), trailer CRC-32",
             "scaling": "strong", "value": round(tb4 / el4_max / GIB, 2), "unit": "GiB/s",
-            "ms_per_step": round(el4_max / args.steps * 1e3, 4), "steps": args.steps,
+            "ms_per_step": round(el4_max / args.steps * 1e3, 4), "steps": args.steps, "warmup_launches": warm4,
             "frames_total": w4["n_total"], "parity_sample_ok": all(r["parity_sample_ok"] for r in pr4),
+            # this rank's (rank 0's) slice against the same box's plain read of the same buffer
+            "roofline": roofline_block(w4["bytes_per_launch"], km4, roof4) if rank == 0 else None,
             "per_rank": pr4, "aggregate_over_max_rank": aggregate(pr4, tb4, el4_max)}
 
     if rank == 0:
@@ -710,6 +861,9 @@ def main():
             "per_rank": per_rank,
             "aggregate_over_max_rank": aggregate(per_rank, total_bytes, elapsed_max),
             **({"cfg4_strong": strong_block} if strong_block is not None else {}),
+            **({"cfg4_strong_proxy": proxy} if proxy is not None else {}),
+            "launcher": os.environ.get("VAL_BENCH_LAUNCHER",
+                                       "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "single process"),
         }
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

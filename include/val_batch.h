@@ -67,6 +67,36 @@
  * (batch_fallbacks): like the provider, the batcher never fails a session
  * over a device error.
  *
+ * Transport failures. A deferred frame's send happens at the window flush,
+ * not in the session's send call: the session counts a staged DATA frame as
+ * sent when it is staged (its `sent` metrics, src/val_core.c:844), and a
+ * send that fails at the flush ends that window (the frames after it are not
+ * sent: tx_unsent) and is returned, once, by the hook call that flushed: the
+ * session's next transport.recv (its ACK wait for that window, so
+ * val_send_files returns VAL_ERR_IO within that window, with detail
+ * RECV_FAILED where the reference records SEND_FAILED), or the send that
+ * stages a control frame or overflows the window (SEND_FAILED). A flush from
+ * transport.flush, which has no status, is reported by the next send or
+ * recv. stats.status names the failure. After it has been reported the
+ * batcher works again: a later val_send_files on the same session runs as on
+ * the bare transport.
+ *
+ * RX answers. The provider answers a call from an RX batch only when its
+ * buffer is the attached recv_buffer, right after the frame's trailer was
+ * delivered, with the frame's length, and with recv_buffer still holding the
+ * frame's 8 header bytes and last CRC-input bytes; anything else (a resume
+ * window read into recv_buffer, src/val_core.c:431-436) is computed directly
+ * (arm_rejects). A header announcing content beyond the MTU stops read-ahead
+ * (the stream's frame boundaries are lost; the session rejects that frame):
+ * the session's reads pass straight through until they have taken one whole
+ * frame the way the session reads frames (header, the content it announces,
+ * trailer), which puts this parser back on the session's frame boundaries;
+ * read-ahead resumes there (resyncs).
+ *
+ * Memory. A direction allocates its window (max_bytes, pinned when a device
+ * was present at attach) when it first batches; until then the RX ring holds
+ * one frame. A batcher with both directions OFF never starts the HIP runtime.
+ *
  * The application keeps its own transport and provider semantics: the
  * wrapped hooks call the ones in the config at attach time (a NULL provider
  * means this library's val_gpu_crc32_provider). Batches below the host-batch
@@ -114,7 +144,12 @@ typedef struct {
     uint64_t rx_batched_answers; /* provider calls answered from an RX batch */
     uint64_t direct_answers;     /* provider calls computed directly (resume windows, split frames) */
     uint64_t batch_fallbacks;    /* batches the GPU path failed and the CPU engine computed (the provider's policy) */
-    int32_t status;              /* first transport or batch failure (VAL_OK if none) */
+    int32_t status;              /* the most recent transport or batch failure (VAL_OK if none) */
+    uint64_t failures;           /* transport or batch failures (each reported once to the session, see below) */
+    uint64_t tx_unsent;          /* staged frames never sent: they followed a failed send in their window */
+    uint64_t arm_rejects;        /* same-length provider calls on recv_buffer whose bytes were not the armed frame
+                                    (computed directly) */
+    uint64_t resyncs;            /* read-ahead resumed after an oversize header (the session's reads framed again) */
 } val_batch_stats_t;
 
 typedef struct val_batch val_batch_t;

@@ -185,6 +185,9 @@ val_status_t val_crc32_verify_frames_host(const uint8_t *base, uint64_t base_len
  * are counted by val_gpu_cpu_batch_count. */
 void val_gpu_set_host_batch_min_bytes(int64_t bytes);
 uint64_t val_gpu_host_batch_min_bytes(void);
+/* The threshold a batch whose mean CRC input per frame is mean_len bytes is
+ * held to (what val_crc32_frames_host applies to it). */
+uint64_t val_gpu_host_batch_min_bytes_for(uint64_t mean_len);
 uint64_t val_gpu_cpu_batch_count(void);
 /* Threads the CPU engine uses for one such batch: the calling thread plus
  * threads - 1 helpers over byte-balanced frame ranges, at most one thread
@@ -192,11 +195,16 @@ uint64_t val_gpu_cpu_batch_count(void);
  * budget (its affinity set capped by the cgroup CPU quota). */
 void val_gpu_set_host_cpu_threads(uint32_t threads);
 /* The *_host_multi calls decide CPU or GPU once for the whole batch: below
- * val_gpu_host_batch_min_bytes() * T / N bytes of CRC input, with N the
- * distinct devices the shards land on and T the CPU engine's threads, the
- * CPU engine answers it. Returns that threshold for
- * `devices` devices. */
+ * val_gpu_host_batch_min_bytes() * T / N_eff bytes of CRC input, with T the
+ * CPU engine's threads, the CPU engine answers it.
+ * N_eff = N, the distinct devices the shards land on, for pinned input;
+ * pageable input also passes through host bounce copies that all shards
+ * share within the process's CPU budget, so N_eff = min(N, the measured
+ * aggregate bounce-copy rate / one GPU's pageable rate). Returns that
+ * threshold for `devices` devices and pageable input (_ex: pinned or not,
+ * and a batch's mean CRC input per frame). */
 uint64_t val_gpu_host_multi_min_bytes(int devices);
+uint64_t val_gpu_host_multi_min_bytes_ex(int devices, int pinned, uint64_t mean_len);
 
 /* Host-memory form of val_crc32_verify_frames_ex_dev (pay: n entries, nullable). */
 val_status_t val_crc32_verify_frames_ex_host(const uint8_t *base, uint64_t base_len, const uint64_t *off,
@@ -263,6 +271,16 @@ void val_gpu_host_free(void *p);
  * calls): one per 4 MiB, at most 8, and all copies together within the
  * process's CPU affinity set. */
 uint32_t val_gpu_host_copy_threads(uint64_t bytes, uint32_t concurrent_copies);
+/* Measurement of the pageable half of the host path, with no device work:
+ * `copies` concurrent copy streams (as the shards of a *_host_multi call),
+ * each copying `bytes` from resident pageable memory into its own bounce
+ * buffer `reps` times through the library's own bounce copy (its thread
+ * policy above). pinned_dst = 1: page-locked destinations (hipHostMalloc, as
+ * the real bounce buffers); 0: malloc'd ones (no HIP runtime needed).
+ * *gbs = copies * reps * bytes / the span from the common start to the last
+ * copy's end, in GB/s. DESIGN.md section 1.3 folds it into the N-device
+ * crossover. */
+val_status_t val_gpu_host_copy_probe(uint32_t copies, uint64_t bytes, uint32_t reps, int pinned_dst, double *gbs);
 /* Wire bytes per H2D chunk of the *_frames_host calls; 0 = default (64 MiB).
  * Device memory use is two chunks. Speed and memory only; results never change. */
 val_status_t val_gpu_set_host_chunk_bytes(size_t bytes);

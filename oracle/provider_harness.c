@@ -114,6 +114,13 @@ static void pipe_init(pipe_t *p, size_t cap)
     pthread_cond_init(&p->cv, NULL);
 }
 
+static void pipe_drain(pipe_t *p)
+{
+    pthread_mutex_lock(&p->mu);
+    p->head = p->len = 0;
+    pthread_mutex_unlock(&p->mu);
+}
+
 static int pipe_push(pipe_t *p, const uint8_t *d, size_t n)
 {
     pthread_mutex_lock(&p->mu);
@@ -212,6 +219,8 @@ typedef struct {
     unsigned long flip_every, data_sent, flipped;  /* fault injection: one payload bit of every Nth DATA frame */
     uint64_t rng;  /* partial-read sizes (VAL_HARNESS_PARTIAL=rN) */
     unsigned long drop_every, data_sent_d, dropped;  /* fault injection: every Nth DATA frame lost */
+    unsigned long fail_at, data_sent_x, send_failures;  /* the fail_at-th DATA frame's send fails, once */
+    unsigned long oversize_at, data_sent_o, oversized;  /* the oversize_at-th DATA frame's content_len -> 0xFFFF */
 } end_t;
 
 /* VAL_HARNESS_FLIP_EVERY=N: the sender's pipe flips one payload bit of every
@@ -237,6 +246,10 @@ static unsigned long drop_every_env(void)
 static int tp_send(void *ctx, const void *data, size_t len)
 {
     end_t *e = (end_t *)ctx;
+    if (e->fail_at && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA && ++e->data_sent_x == e->fail_at) {
+        e->send_failures++;
+        return -1;  /* the transport refused this frame: nothing went on the wire */
+    }
     e->digest = val_crc32_update_state(e->digest, data, len);
     e->frames++;
     if (e->caplog) {
@@ -254,6 +267,17 @@ static int tp_send(void *ctx, const void *data, size_t len)
         ++e->data_sent_d % e->drop_every == 0) {
         e->dropped++;
         return (int)len;  /* "sent": lost on the way */
+    }
+    if (e->oversize_at && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA && ++e->data_sent_o == e->oversize_at) {
+        /* a header whose content_len exceeds any MTU: the receiver rejects it
+           (src/val_core.c:915-921) and reads the rest of the frame as data */
+        uint8_t *c = (uint8_t *)malloc(len);
+        memcpy(c, data, len);
+        c[2] = c[3] = 0xFF;
+        e->oversized++;
+        const int rc = pipe_push(e->out, c, len);
+        free(c);
+        return rc;
     }
     if (e->flip_every && len > 20 && ((const uint8_t *)data)[0] == VAL_PKT_DATA &&
         ++e->data_sent % e->flip_every == 0) {
@@ -304,6 +328,30 @@ static int tp_recv(void *ctx, void *buffer, size_t size, size_t *got, uint32_t t
     return 0;
 }
 
+/* VAL_HARNESS_STALE_ARM=1 (batched loopback): before each of the receiver's
+ * frame checks the provider is first called on recv_buffer holding other
+ * bytes of the same length (as a resume window read into recv_buffer leaves
+ * it, src/val_core.c:431-436) while the batcher has the real frame's CRC
+ * armed: the answer must be those bytes' CRC. Then the real call. */
+static crc32_func_t g_stale_real;
+static const void *g_stale_buf;
+static unsigned long g_stale_probes, g_stale_wrong;
+static uint32_t stale_probe_provider(uint32_t seed, const void *buf, size_t len)
+{
+    if (buf == g_stale_buf && seed == 0xFFFFFFFFu && len >= 8) {
+        uint8_t *p = (uint8_t *)buf;
+        uint8_t *save = (uint8_t *)malloc(len);
+        memcpy(save, p, len);
+        oracle_prng_fill(0x57A1Eu + g_stale_probes, p, len);
+        const uint32_t want = val_crc32(p, len);
+        g_stale_wrong += g_stale_real(seed, p, len) != want;
+        g_stale_probes++;
+        memcpy(p, save, len);
+        free(save);
+    }
+    return g_stale_real(seed, buf, len);
+}
+
 static void *fs_open(void *c, const char *path, const char *mode) { (void)c; return fopen(path, mode); }
 static size_t fs_read(void *c, void *b, size_t s, size_t n, void *f) { (void)c; return fread(b, s, n, (FILE *)f); }
 static size_t fs_write(void *c, const void *b, size_t s, size_t n, void *f) { (void)c; return fwrite(b, s, n, (FILE *)f); }
@@ -333,6 +381,18 @@ static void make_cfg(val_config_t *cfg, end_t *e, size_t mtu, crc32_func_t prov)
     cfg->resume.tail_cap_bytes = 1024;
     cfg->timeouts.min_timeout_ms = 200;
     cfg->timeouts.max_timeout_ms = 5000;
+    /* VAL_HARNESS_MIN_TIMEOUT_MS: a floor that a loaded test host's scheduling
+       stalls never reach (runs that compare wire bytes across transports) */
+    if (getenv("VAL_HARNESS_MIN_TIMEOUT_MS")) {
+        cfg->timeouts.min_timeout_ms = (uint32_t)atoi(getenv("VAL_HARNESS_MIN_TIMEOUT_MS"));
+        if (cfg->timeouts.max_timeout_ms < cfg->timeouts.min_timeout_ms) cfg->timeouts.max_timeout_ms = cfg->timeouts.min_timeout_ms;
+    }
+    /* VAL_HARNESS_MAX_TIMEOUT_MS: a lower ceiling, so a receiver whose peer has
+       gone gives up sooner (sendfail) */
+    if (getenv("VAL_HARNESS_MAX_TIMEOUT_MS")) {
+        const uint32_t m = (uint32_t)atoi(getenv("VAL_HARNESS_MAX_TIMEOUT_MS"));
+        cfg->timeouts.max_timeout_ms = m > cfg->timeouts.min_timeout_ms ? m : cfg->timeouts.min_timeout_ms;
+    }
     cfg->retries.handshake_retries = 3;
     cfg->retries.meta_retries = 2;
     cfg->retries.data_retries = 4;
@@ -447,6 +507,7 @@ typedef struct {
     uint64_t tx_frames, tx_batched_frames, tx_batches, tx_max_batch, rx_frames, rx_batches, rx_max_batch,
         rx_batched_answers, direct_answers, batch_fallbacks;
     int32_t status;
+    uint64_t failures, tx_unsent, arm_rejects, resyncs;
 } hb_stats_t;
 typedef int (*fn_battach_t)(val_config_t *, const hb_opts_t *, void **);
 typedef void (*fn_bdetach_t)(void *);
@@ -489,13 +550,16 @@ static void batch_report(FILE *out, void *ba, void *bb)
     for (int k = 0; k < 2; k++)
         fprintf(out, "%s{\"end\":\"%s\",\"tx_frames\":%llu,\"tx_batched_frames\":%llu,\"tx_batches\":%llu,\"tx_max_batch\":%llu,"
                "\"rx_frames\":%llu,\"rx_batches\":%llu,\"rx_max_batch\":%llu,\"rx_batched_answers\":%llu,"
-               "\"direct_answers\":%llu,\"batch_fallbacks\":%llu,\"status\":%d}",
+               "\"direct_answers\":%llu,\"batch_fallbacks\":%llu,\"status\":%d,\"failures\":%llu,\"tx_unsent\":%llu,"
+               "\"arm_rejects\":%llu,\"resyncs\":%llu}",
                k ? "," : "", k ? "receiver" : "sender", (unsigned long long)st[k].tx_frames,
                (unsigned long long)st[k].tx_batched_frames, (unsigned long long)st[k].tx_batches,
                (unsigned long long)st[k].tx_max_batch, (unsigned long long)st[k].rx_frames,
                (unsigned long long)st[k].rx_batches, (unsigned long long)st[k].rx_max_batch,
                (unsigned long long)st[k].rx_batched_answers, (unsigned long long)st[k].direct_answers,
-               (unsigned long long)st[k].batch_fallbacks, st[k].status);
+               (unsigned long long)st[k].batch_fallbacks, st[k].status, (unsigned long long)st[k].failures,
+               (unsigned long long)st[k].tx_unsent, (unsigned long long)st[k].arm_rejects,
+               (unsigned long long)st[k].resyncs);
     fprintf(out, "]");
     dt(ba);
     dt(bb);
@@ -814,6 +878,7 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     erx.log = (frame_rec_t *)malloc(erx.caplog * sizeof(frame_rec_t));
     etx.flip_every = flip_every_env();
     etx.drop_every = drop_every_env();
+    etx.oversize_at = getenv("VAL_HARNESS_OVERSIZE_AT") ? strtoul(getenv("VAL_HARNESS_OVERSIZE_AT"), NULL, 0) : 0ul;
     etx.rng = g_seed * 2u + 1u;  /* partial-read draws (VAL_HARNESS_PARTIAL=rN), per end */
     erx.rng = g_seed * 2u + 2u;
     crc32_func_t prov = use_gpu ? counting_provider : NULL;
@@ -828,6 +893,12 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     const uint64_t cpu_b0 = lib_count("val_gpu_cpu_batch_count"), cpu_s0 = lib_count("val_gpu_cpu_small_count"),
                    cpu_f0 = lib_count("val_gpu_cpu_fallback_count");
     if (batched && batch_attach(&ctx_, &crx, &ba, &bb) != 0) return 4;
+    const int stale = batched && getenv("VAL_HARNESS_STALE_ARM") && atoi(getenv("VAL_HARNESS_STALE_ARM"));
+    if (stale) {  /* the receiver's provider, wrapped before its session copies the config */
+        g_stale_real = crx.crc32_provider;
+        g_stale_buf = crx.buffers.recv_buffer;
+        crx.crc32_provider = stale_probe_provider;
+    }
     val_session_t *tx = NULL, *rx = NULL;
     if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
     rx_job_t job = {rx, outdir, VAL_OK};
@@ -857,22 +928,129 @@ static int loopback_run(FILE *out_json, size_t bytes, size_t mtu, int use_gpu, u
     fprintf(out_json, "{\"mode\":\"loopback\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"tx_status\":%d,"
            "\"rx_status\":%d,\"equal\":%d,"
            "\"tx_crc_errors\":%u,\"rx_crc_errors\":%u,\"retransmits\":%u,\"timeouts\":%u,\"tx_frames\":%lu,\"rx_frames\":%lu,"
-           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"wire_frames\":%lu,\"flipped\":%lu,\"dropped\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
-           "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu",
+           "\"tx_digest\":%u,\"rx_digest\":%u,\"trailers_ok\":%lu,\"wire_frames\":%lu,\"flipped\":%lu,\"dropped\":%lu,\"oversized\":%lu,\"provider_calls\":%lu,\"wall_ms\":%u,"
+           "\"lib_cpu_batches\":%llu,\"lib_cpu_small\":%llu,\"lib_cpu_fallbacks\":%llu,\"stale_probes\":%lu,"
+           "\"stale_wrong\":%lu",
            use_gpu, batched, window, bytes, mtu, st, job.st, equal, mt.crc_errors, mr.crc_errors, mt.retransmits + mr.retransmits,
            mt.timeouts + mr.timeouts, etx.frames, erx.frames, etx.digest ^ 0xFFFFFFFFu, erx.digest ^ 0xFFFFFFFFu,
-           t_ok, wf_tx + wf_rx, etx.flipped, etx.dropped, __atomic_load_n(&g_calls, __ATOMIC_RELAXED), t1 - t0,
+           t_ok, wf_tx + wf_rx, etx.flipped, etx.dropped, etx.oversized, __atomic_load_n(&g_calls, __ATOMIC_RELAXED), t1 - t0,
            (unsigned long long)(lib_count("val_gpu_cpu_batch_count") - cpu_b0),
            (unsigned long long)(lib_count("val_gpu_cpu_small_count") - cpu_s0),
-           (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0));
+           (unsigned long long)(lib_count("val_gpu_cpu_fallback_count") - cpu_f0), stale ? g_stale_probes : 0ul,
+           stale ? g_stale_wrong : 0ul);
     val_session_destroy(tx);
     val_session_destroy(rx);
+    if (stale) crx.crc32_provider = g_stale_real;  /* detach restores what attach saw */
     if (batched) batch_report(out_json, ba, bb);
     fprintf(out_json, "}\n");
     for (size_t i = 0; i < etx.nlog; i++) free(etx.log[i].bytes);
     for (size_t i = 0; i < erx.nlog; i++) free(erx.log[i].bytes);
     free(etx.log);
     free(erx.log);
+    free(data);
+    remove(out);
+    remove(in);
+    rmdir(outdir);
+    rmdir(dir);
+    return 0;
+}
+
+/* provider_harness <lib|none> sendfail|oversize <bytes> <mtu> <window> <k> [batched]
+ * Two transfers on one pair of sessions; a fault in the first, the second
+ * clean. sendfail: the sender's transport fails the k-th DATA frame's send
+ * (once); in the reference val_send_files returns VAL_ERR_IO at that frame
+ * (src/val_core.c:835-842, src/val_sender.c:835-840) and the receiver's
+ * transfer ends on its own timeouts. oversize: the k-th DATA frame arrives
+ * with content_len 0xFFFF; the receiver rejects it (src/val_core.c:915-921)
+ * and, in the reference, that transfer fails. The second transfer resumes the
+ * receiver's partial file (VAL_RESUME_TAIL). Prints both transfers'
+ * statuses, the sender's last error detail, its wire digest and frames at
+ * the end of the first, and whether the second transfer's file arrived
+ * whole. */
+static int mode_twice(size_t bytes, size_t mtu, int use_gpu, uint16_t window, int oversize, unsigned long k, int batched)
+{
+    char tmpl[] = "/tmp/valfailXXXXXX";
+    char *dir = mkdtemp(tmpl);
+    if (!dir) return 2;
+    char in[512], outdir[512], out[512];
+    snprintf(in, sizeof in, "%s/input.bin", dir);
+    snprintf(outdir, sizeof outdir, "%s/out", dir);
+    snprintf(out, sizeof out, "%s/out/input.bin", dir);
+    mkdir(outdir, 0777);
+    uint8_t *data = (uint8_t *)malloc(bytes ? bytes : 1);
+    oracle_prng_fill(0xFA11u, data, bytes);
+    FILE *f = fopen(in, "wb");
+    fwrite(data, 1, bytes, f);
+    fclose(f);
+    pipe_t a2b, b2a;
+    const size_t pwin = (size_t)2u * (window ? window : 1u) * mtu + ((size_t)1u << 20);
+    const size_t pcap = pwin > ((size_t)64u << 20) ? pwin : ((size_t)64u << 20);
+    pipe_init(&a2b, pcap);
+    pipe_init(&b2a, pcap);
+    end_t etx, erx;
+    memset(&etx, 0, sizeof etx);
+    memset(&erx, 0, sizeof erx);
+    etx.out = &a2b;
+    etx.in = &b2a;
+    erx.out = &b2a;
+    erx.in = &a2b;
+    etx.digest = erx.digest = 0xFFFFFFFFu;
+    if (oversize) etx.oversize_at = k;
+    else etx.fail_at = k;
+    val_config_t ctx_, crx;
+    make_cfg(&ctx_, &etx, mtu, use_gpu ? counting_provider : NULL);
+    make_cfg(&crx, &erx, mtu, use_gpu ? counting_provider : NULL);
+    if (window) {
+        ctx_.tx_flow.window_cap_packets = crx.tx_flow.window_cap_packets = window;
+        ctx_.tx_flow.initial_cwnd_packets = crx.tx_flow.initial_cwnd_packets = window;
+    }
+    void *ba = NULL, *bb = NULL;
+    if (batched && batch_attach(&ctx_, &crx, &ba, &bb) != 0) return 4;
+    val_session_t *tx = NULL, *rx = NULL;
+    if (val_session_create(&ctx_, &tx, NULL) != VAL_OK || val_session_create(&crx, &rx, NULL) != VAL_OK) return 3;
+    const char *files[1] = {in};
+    val_status_t st[2], rst[2], code = VAL_OK;
+    uint32_t detail = 0;
+    uint32_t digest1 = 0;
+    unsigned long frames1 = 0;
+    for (int t = 0; t < 2; t++) {
+        rx_job_t job = {rx, outdir, VAL_OK};
+        pthread_t th;
+        pthread_create(&th, NULL, rx_main, &job);
+        st[t] = val_send_files(tx, files, 1, NULL);
+        if (t == 0) {
+            val_get_last_error(tx, &code, &detail);
+            digest1 = etx.digest ^ 0xFFFFFFFFu;
+            frames1 = etx.frames;
+            etx.fail_at = etx.oversize_at = 0;  /* the second transfer runs clean */
+        }
+        pthread_join(th, NULL);
+        rst[t] = job.st;
+        if (t == 0 && oversize) {
+            /* after a protocol error the application reconnects: the old
+               connection's bytes are gone (both directions) */
+            pipe_drain(&a2b);
+            pipe_drain(&b2a);
+        }
+    }
+    int equal = 0;
+    FILE *g = fopen(out, "rb");
+    if (g) {
+        uint8_t *back = (uint8_t *)malloc(bytes + 1);
+        size_t r = fread(back, 1, bytes + 1, g);
+        fclose(g);
+        equal = (r == bytes) && memcmp(back, data, bytes) == 0;
+        free(back);
+    }
+    printf("{\"mode\":\"%s\",\"gpu\":%d,\"batched\":%d,\"window\":%u,\"bytes\":%zu,\"mtu\":%zu,\"fail_at\":%lu,"
+           "\"tx_status1\":%d,\"rx_status1\":%d,\"tx_error1\":%d,\"tx_detail1\":%u,\"tx_digest1\":%u,\"tx_frames1\":%lu,"
+           "\"send_failures\":%lu,\"tx_status2\":%d,\"rx_status2\":%d,\"equal2\":%d",
+           oversize ? "oversize" : "sendfail", use_gpu, batched, window, bytes, mtu, k, st[0], rst[0], code, detail, digest1, frames1, etx.send_failures, st[1],
+           rst[1], equal);
+    val_session_destroy(tx);
+    val_session_destroy(rx);
+    if (batched) batch_report(stdout, ba, bb);
+    printf("}\n");
     free(data);
     remove(out);
     remove(in);
@@ -1480,6 +1658,10 @@ int main(int argc, char **argv)
         return use_gpu ? mode_loopback_par((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0),
                                            (uint16_t)strtoul(argv[5], NULL, 0), atoi(argv[6]))
                        : 1;
+    if ((!strcmp(argv[2], "sendfail") || !strcmp(argv[2], "oversize")) && argc >= 7)
+        return mode_twice((size_t)strtoull(argv[3], NULL, 0), (size_t)strtoull(argv[4], NULL, 0), use_gpu,
+                          (uint16_t)strtoul(argv[5], NULL, 0), !strcmp(argv[2], "oversize"), strtoul(argv[6], NULL, 0),
+                          argc >= 8 && use_gpu ? atoi(argv[7]) : 0);
     if (!strcmp(argv[2], "sessions")) return use_gpu ? mode_sessions(counting_provider, 0) : 1;
     if (!strcmp(argv[2], "sessions-batched")) return use_gpu ? mode_sessions(counting_provider, 1) : 1;
     fprintf(stderr, "bad mode\n");

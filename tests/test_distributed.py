@@ -124,3 +124,39 @@ def test_bench_refuses_more_ranks_than_gpus():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2, (r.returncode, r.stderr[-1000:])
     assert "need 2 visible GPUs" in r.stderr and r.stdout == ""
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    """A launcher that started a different number of ranks than --gpus asks
+    for: bench.py exits non-zero with a message before importing torch."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stderr[-1000:])
+    assert "--gpus 4 but WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_bench_gpus_n_starts_ranks_itself():
+    """`bench.py --gpus N` without torchrun: the ranks are started as a fresh
+    child process (torch.distributed.run over 127.0.0.1, the same script and
+    arguments), decided before any GPU call; with the nccl backend and fewer
+    visible GPUs than N (none here) the parent refuses with exit 2 first."""
+    import subprocess
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cmd = bench.rank_launch_command(8, ["--gpus", "8", "--steps", "3"], 29500)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8" and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29500"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "VAL_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stderr[-1000:])
+    assert "--gpus 8 needs 8 visible GPUs" in r.stderr and r.stdout == ""

@@ -70,15 +70,27 @@ def test_bench_two_ranks_weak_cfg2():
     assert st["value"] > 0
 
 
-def test_bench_eight_ranks_rehearsal():
-    """The driver's 8-GPU invocation rehearsed on one GPU: 8 ranks under
-    torch.distributed.run (gloo for the host-side collectives, all on
-    cuda:0), cfg2 weak plus the cfg4 strong block: the 8 GiB file's 131,113
+def test_bench_eight_ranks_driver_command():
+    """The driver's 8-GPU invocation, literally: `python3 bench.py --gpus 8 ...`
+    with no torchrun around it. bench.py starts the 8 ranks itself (a
+    torch.distributed.run child process, decided before any GPU call), here
+    rehearsed on one GPU (gloo for the host-side collectives, all ranks on
+    cuda:0): cfg2 weak plus the cfg4 strong block, the 8 GiB file's 131,113
     frames split byte-balanced (~16,389 per rank, no collective on the data),
     the 816-B last frame on rank 7, the aggregate over the slowest rank, and
     every rank's parity sample against the oracle."""
-    line = _bench_two_ranks("cfg2", "--with-cfg4-strong", "--no-host-inclusive", ranks=8, timeout=170)
+    env = dict(os.environ, VAL_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--config", "cfg2", "--with-cfg4-strong",
+           "--no-host-inclusive", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints exactly one line, through the parent's stdout
+    line = json.loads(lines[0])
+    assert line["launcher"].startswith("bench.py --gpus")
     assert line["n_gpus"] == 8 and line["scaling"] == "weak" and line["config"]["parity_sample_ok"] is True
+    assert line["cpu_baseline"] is None and "cfg4_strong_proxy" not in line  # N > 1: measured ranks, no proxy
     pr = line["per_rank"]
     assert [r["rank"] for r in pr] == list(range(8)) and all(r["parity_sample_ok"] for r in pr)
     assert line["aggregate_over_max_rank"]["total_bytes"] == 8 * 2 * 65536 * (8 + 8 + 1024)
@@ -94,6 +106,34 @@ def test_bench_eight_ranks_rehearsal():
     assert agg["total_bytes"] == 2 * file_crc_input
     assert agg["max_elapsed_s"] == max(r["elapsed_s"] for r in spr)
     assert abs(st["value"] - agg["total_bytes"] / agg["max_elapsed_s"] / 2**30) / st["value"] < 0.01
+    assert st["roofline"]["frac"] > 0 and st["roofline"]["bytes_per_launch"] == spr[0]["bytes_per_step"]
+
+
+def test_bench_cfg4_proxy_at_one_gpu():
+    """N = 1: after the cfg4 block, the single-GPU proxy of the 2/4/8-GPU
+    strong-scaling curve: for each N the largest slice and the last rank's
+    slice (the 816-B frame) of the file as N ranks split it, each timed alone
+    and parity-sampled against the oracle."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg2", "--with-cfg4-strong",
+           "--no-host-inclusive", "--no-cpu-baseline", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    px = line["cfg4_strong_proxy"]
+    assert px["parity_sample_ok"] is True and "single-GPU proxy" in px["label"]
+    file_crc_input = 131112 * (8 + 8 + 65516) + 8 + 8 + 800
+    assert px["file_crc_input_bytes"] == file_crc_input
+    assert px["1"]["frames"] == 131113
+    for n in (2, 4, 8):
+        sl = px[str(n)]["slices_timed"]
+        assert sl[-1]["rank"] == n - 1 and sl[-1]["last_frame_crc_input"] == 8 + 8 + 800
+        assert all(s["parity_sample_ok"] and s["kernel_ms"] > 0 for s in sl)
+        assert 131113 // n - 2 <= max(s["frames"] for s in sl) <= 131113 // n + 2
+        assert px[str(n)]["est_aggregate_GiB_s"] > 0
+    rf = line["cfg4_strong"]["roofline"]
+    assert rf["bytes_per_launch"] == file_crc_input and rf["read_roof"] and rf["frac_of_read_roof"] > 0
 
 
 def test_bench_rccl_process_group_one_rank():

@@ -162,17 +162,41 @@ def _cpu_budget() -> int:
     return n
 
 
+def _n_eff_x16(n: int, pinned: bool) -> int:
+    """The N-device rule restated: pinned input
+    scales with N; pageable input is capped by the host bounce copies, which
+    all shards share within the CPU budget: one copy thread ~14 GB/s, all
+    copies together ~135 GB/s, against ~53 GB/s per GPU's pageable path
+    (profiles/r06_bounce_copy_scaling.jsonl)."""
+    if pinned:
+        return 16 * n
+    per_copy = max(1, min(8, max(1, _cpu_budget() // n), 16))  # val_gpu_host_copy_threads(64 MiB, n)
+    assert per_copy == vc.lib().val_gpu_host_copy_threads(64 << 20, n)
+    copy = min(min(_cpu_budget(), n * per_copy) * 14000, 135000)
+    return max(16, min(16 * n, copy * 16 // 53000))
+
+
 def test_multi_decides_once_for_the_whole_batch():
     """val_crc32_*_host_multi choose CPU or GPU once per batch against a
     crossover that scales with the distinct devices and the CPU threads
-    (C1 * T / N), never per shard; below it the batch needs no device (this
-    container has none) and the helper threads stay within the CPU budget."""
+    (C1 * T / N_eff; N_eff = N for pinned input, capped by the shared host
+    bounce copies for pageable input), never per shard; below it the batch
+    needs no device (this container has none) and the helper threads stay
+    within the CPU budget."""
     vc.set_host_batch_min_bytes(64 << 20)  # the built-in single-GPU crossover (conftest exports 0)
+    c1 = 64 << 20
     try:
-        assert vc.host_multi_min_bytes(1) == 64 << 20
-        assert vc.host_multi_min_bytes(8) == 8 << 20
+        assert vc.host_multi_min_bytes(1) == c1
+        for n in (1, 2, 4, 8):
+            assert vc.host_multi_min_bytes(n, pinned=True) == c1 // n
+            assert vc.host_multi_min_bytes(n, pinned=False) == c1 * 16 // _n_eff_x16(n, False), n
+            assert vc.host_multi_min_bytes(n) == vc.host_multi_min_bytes(n, pinned=False)
+        # pageable shards never reach more devices' worth of GPU than the copies feed
+        assert vc.host_multi_min_bytes(8, pinned=False) >= vc.host_multi_min_bytes(8, pinned=True)
+        if _cpu_budget() >= 16:  # the GPU box's share: N_eff 2.55 from 4 devices on
+            assert _n_eff_x16(8, False) == 40 and _n_eff_x16(2, False) == 32
         vc.set_host_cpu_threads(4)
-        assert vc.host_multi_min_bytes(8) == min(4, _cpu_budget()) * (8 << 20)
+        assert vc.host_multi_min_bytes(8, pinned=True) == min(4, _cpu_budget()) * (c1 // 8)
         vc.set_host_cpu_threads(1)
         n, flen, stride = 2000, 1040, 1044
         sb = _prng.prng_bytes(97, n * stride)

@@ -54,9 +54,10 @@ EXPORTS = (
     "val_frame_payload_lens", "val_gpu_set_provider_min_bytes", "val_gpu_provider_min_bytes",
     "val_gpu_cpu_small_count", "val_gpu_last_hook_path", "val_crc32_cpu_update_state", "val_crc32_cpu_engine",
     "val_crc32_fold_payload_states_at", "val_frame_data_offsets", "val_gpu_build_flags",
-    "val_gpu_host_copy_threads", "val_gpu_set_ragged_min_frames", "val_gpu_ragged_min_frames",
+    "val_gpu_host_copy_threads", "val_gpu_host_copy_probe", "val_gpu_set_ragged_min_frames", "val_gpu_ragged_min_frames",
     "val_gpu_scratch_entries", "val_gpu_set_host_batch_min_bytes", "val_gpu_host_batch_min_bytes",
-    "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads", "val_gpu_host_multi_min_bytes",
+    "val_gpu_host_batch_min_bytes_for",
+    "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads", "val_gpu_host_multi_min_bytes", "val_gpu_host_multi_min_bytes_ex",
     "val_batch_attach", "val_batch_flush", "val_batch_get_stats", "val_batch_detach", "val_batch_crc32_provider",
     "val_serialize_handshake", "val_deserialize_handshake", "val_serialize_meta", "val_deserialize_meta",
     "val_serialize_resume_resp", "val_deserialize_resume_resp", "val_serialize_verify_request",
@@ -147,14 +148,17 @@ def _declare(lib: ctypes.CDLL, strict: bool = True) -> None:
     fn("val_frame_data_offsets", None, _vp, _vp, _vp, u32, _vp)
     fn("val_gpu_build_flags", ctypes.c_char_p)
     fn("val_gpu_host_copy_threads", u32, u64, u32)
+    fn("val_gpu_host_copy_probe", i32, u32, u64, u32, ctypes.c_int, ctypes.POINTER(ctypes.c_double))
     fn("val_gpu_set_ragged_min_frames", None, ctypes.c_int64)
     fn("val_gpu_ragged_min_frames", u32)
     fn("val_gpu_scratch_entries", u32, ctypes.c_int, ctypes.POINTER(u64))
     fn("val_gpu_set_host_batch_min_bytes", None, ctypes.c_int64)
     fn("val_gpu_host_batch_min_bytes", u64)
+    fn("val_gpu_host_batch_min_bytes_for", u64, u64)
     fn("val_gpu_cpu_batch_count", u64)
     fn("val_gpu_set_host_cpu_threads", None, u32)
     fn("val_gpu_host_multi_min_bytes", u64, ctypes.c_int)
+    fn("val_gpu_host_multi_min_bytes_ex", u64, ctypes.c_int, ctypes.c_int, u64)
 
 
 def lib() -> ctypes.CDLL:
@@ -268,10 +272,22 @@ def set_host_cpu_threads(threads: int) -> None:
     lib().val_gpu_set_host_cpu_threads(int(threads))
 
 
-def host_multi_min_bytes(devices: int) -> int:
+def host_multi_min_bytes(devices: int, pinned: Optional[bool] = None, mean_len: int = 2**64 - 1) -> int:
     """CRC-input bytes below which a *_host_multi batch over `devices`
-    distinct GPUs is answered by the CPU engine (decided once per batch)."""
-    return int(lib().val_gpu_host_multi_min_bytes(int(devices)))
+    distinct GPUs is answered by the CPU engine (decided once per batch);
+    pageable input unless `pinned`."""
+    if pinned is None:
+        return int(lib().val_gpu_host_multi_min_bytes(int(devices)))
+    return int(lib().val_gpu_host_multi_min_bytes_ex(int(devices), 1 if pinned else 0, int(mean_len)))
+
+
+def host_copy_probe(copies: int, nbytes: int, reps: int, pinned: bool = True) -> float:
+    """Aggregate GB/s of `copies` concurrent pageable-to-bounce copies through
+    the library's own bounce copy (val_gpu_host_copy_probe); no device work."""
+    g = ctypes.c_double(0.0)
+    _check(lib().val_gpu_host_copy_probe(copies, nbytes, reps, 1 if pinned else 0, ctypes.byref(g)),
+           "val_gpu_host_copy_probe")
+    return float(g.value)
 
 
 def set_ragged_min_frames(frames: int) -> None:

@@ -42,15 +42,18 @@ struct val_batch {
     uint32_t win_cap;        /* the config's window cap in frames (0 in the config = 1, src/val_core.c:1755) */
     int pinned;              /* allocate windows pinned (a device is present) */
     int tx_pinned, rx_pinned; /* how each window buffer was allocated */
-    /* TX window */
+    int err;                 /* a failure no hook call has reported to the session yet (transport.flush has no
+                                status): the next send or recv reports it, once */
+    /* TX window: allocated when TX first batches */
     uint8_t *tx;
+    size_t tx_cap;
     size_t tx_used;
     vb_frame_t *txf;
     uint32_t tx_n;
     size_t tx_pending;  /* CRC input of the frame whose placeholder was just returned (0: none) */
     /* RX ring: bytes [r_head, r_len) not yet handed to the session */
     uint8_t *rx;
-    size_t rx_cap;  /* the ring's bytes: max_bytes with read-ahead, else one frame */
+    size_t rx_cap;  /* the ring's bytes: one frame until RX first batches, then max_bytes */
     size_t r_head, r_len;
     vb_frame_t *rxf;
     uint32_t rx_n, rx_cur;  /* complete frames in the ring; the one being delivered */
@@ -62,12 +65,21 @@ struct val_batch {
     size_t hdr_have;
     uint32_t cur_len;  /* CRC input of the frame in progress (its header is complete) */
     uint32_t (*ticks)(void);  /* the config's clock (val_config_t.system.get_ticks_ms), for read deadlines */
-    int raw;  /* a header announced content beyond the MTU: no more read-ahead */
+    int raw;  /* a header announced content beyond the MTU: read-ahead stops until the session's own reads
+                 show it at a frame boundary again (rs_*) */
+    int rs_seg;             /* while raw: the segment the session is reading (0 header, 1 content, 2 trailer;
+                               -1 unknown) */
+    size_t rs_left;         /* its bytes still to come */
+    uint8_t rs_hdr[VAL_WIRE_HEADER_SIZE];
     /* delivery of frame rx_cur into recv_buffer in place */
     size_t cur_matched;
     int armed;
     uint32_t armed_len, armed_crc;
+    uint8_t armed_head[VAL_WIRE_HEADER_SIZE];  /* the armed frame's header and last CRC-input bytes: the */
+    uint8_t armed_tail[8];                      /* provider answers from the batch only for these bytes */
+    uint32_t armed_tail_n;
     val_batch_stats_t st;
+    /* per-frame arrays, allocated with the first window buffer */
     uint32_t *crc_tmp;
     uint64_t *off_tmp;
     uint32_t *len_tmp;
@@ -127,11 +139,13 @@ static uint32_t vb_direct(val_batch_t *b, uint32_t seed, const void *buf, size_t
 
 static void vb_fail(val_batch_t *b, val_status_t st)
 {
-    if (b->st.status == VAL_OK) b->st.status = st;
+    b->st.status = st;
+    b->st.failures++;
 }
 
-/* Whether a direction batches now (include/val_batch.h, "When batching
- * pays"): its largest possible batch against the host-batch crossover. */
+/* The host-batch crossover for this session's frames: their mean CRC input
+ * is about one MTU, so AUTO decides as val_crc32_frames_host will for the
+ * batch it would send (val_gpu_host_batch_min_bytes_for). */
 static int vb_engaged(const val_batch_t *b, int mode)
 {
     if (mode == VAL_BATCH_ALWAYS) return 1;
@@ -139,7 +153,82 @@ static int vb_engaged(const val_batch_t *b, int mode)
     if (!b->pinned) return 0;  /* no device at attach: every batch would run on the CPU engine */
     uint64_t ub = (uint64_t)b->win_cap * b->mtu;
     if (ub > b->opt.max_bytes) ub = b->opt.max_bytes;
-    return ub >= val_gpu_host_batch_min_bytes();
+    return ub >= val_gpu_host_batch_min_bytes_for(b->mtu - VAL_WIRE_TRAILER_SIZE);
+}
+
+static void *vb_alloc(const val_batch_t *b, size_t n, int *pinned)
+{
+    void *p = b->pinned ? val_gpu_host_alloc(n) : NULL;
+    *pinned = p != NULL;
+    return p ? p : malloc(n);
+}
+
+static void vb_free(void *p, int pinned)
+{
+    if (!p) return;
+    if (pinned) val_gpu_host_free(p);
+    else free(p);
+}
+
+/* The per-frame arrays both directions share, on first use. */
+static int vb_frames_ready(val_batch_t *b)
+{
+    if (b->crc_tmp) return 1;
+    const uint32_t nf = b->opt.max_frames;
+    uint32_t *c = (uint32_t *)calloc(nf, sizeof(uint32_t));
+    uint64_t *o = (uint64_t *)calloc(nf, sizeof(uint64_t));
+    uint32_t *l = (uint32_t *)calloc(nf, sizeof(uint32_t));
+    if (!c || !o || !l) {
+        free(c);
+        free(o);
+        free(l);
+        return 0;
+    }
+    b->crc_tmp = c;
+    b->off_tmp = o;
+    b->len_tmp = l;
+    return 1;
+}
+
+/* The TX window, allocated when TX first batches (a session whose windows
+ * never reach the crossover pins nothing). 0: no memory; the frame is then
+ * hashed by the provider and sent at once. */
+static int vb_tx_ready(val_batch_t *b)
+{
+    if (b->tx) return 1;
+    if (!vb_frames_ready(b)) return 0;
+    vb_frame_t *f = (vb_frame_t *)calloc(b->opt.max_frames, sizeof(vb_frame_t));
+    uint8_t *w = f ? (uint8_t *)vb_alloc(b, b->opt.max_bytes, &b->tx_pinned) : NULL;
+    if (!w) {
+        free(f);
+        return 0;
+    }
+    b->txf = f;
+    b->tx = w;
+    b->tx_cap = b->opt.max_bytes;
+    return 1;
+}
+
+/* The RX ring grown from one frame to a batch window when RX first batches;
+ * called only with the ring empty. 0: no memory (this fill reads one frame). */
+static int vb_rx_ready(val_batch_t *b)
+{
+    if (b->rxf && b->rx_cap >= b->opt.max_bytes) return 1;
+    if (!vb_frames_ready(b)) return 0;
+    vb_frame_t *f = (vb_frame_t *)calloc(b->opt.max_frames, sizeof(vb_frame_t));
+    int pinned = 0;
+    uint8_t *r = f ? (uint8_t *)vb_alloc(b, b->opt.max_bytes, &pinned) : NULL;
+    if (!r) {
+        free(f);
+        return 0;
+    }
+    memcpy(r, b->rx, b->r_len);  /* bytes of a frame in progress (none at a fill's start) */
+    vb_free(b->rx, b->rx_pinned);
+    b->rx = r;
+    b->rx_pinned = pinned;
+    b->rx_cap = b->opt.max_bytes;
+    b->rxf = f;
+    return 1;
 }
 
 static int vb_tx_engaged(const val_batch_t *b)
@@ -174,13 +263,20 @@ static val_status_t vb_hash(val_batch_t *b, const uint8_t *buf, size_t used, vb_
 }
 
 /* ---- TX ---------------------------------------------------------------- */
+/* Send the staged window: trailers from one batch, then the frames in order.
+ * A transport send that fails ends the window there: the frames after it are
+ * not sent (tx_unsent), as the reference's sender stops at the frame whose
+ * send failed (src/val_core.c:835-842, src/val_sender.c:835-840). The
+ * failure is returned to this call only (the caller reports it to the
+ * session once); the batcher itself stays usable for later transfers. */
 static val_status_t vb_flush_tx(val_batch_t *b)
 {
-    if (!b->tx_n) return b->st.status;
+    if (!b->tx_n) return VAL_OK;
     uint32_t need = 0;
     for (uint32_t i = 0; i < b->tx_n; i++) need += b->txf[i].need;
-    val_status_t st = b->st.status;
-    if (st == VAL_OK && need) {
+    val_status_t st = VAL_OK;
+    uint32_t sent = 0;
+    if (need) {
         st = vb_hash(b, b->tx, b->tx_used, b->txf, b->tx_n, 1);
         if (st == VAL_OK) {
             b->st.tx_batches++;
@@ -201,18 +297,32 @@ static val_status_t vb_flush_tx(val_batch_t *b)
     }
     if (st == VAL_OK) {
         if (b->opt.coalesce_send) {
-            if (b->u_send(b->u_io, b->tx, b->tx_used) != (int)b->tx_used) vb_fail(b, st = VAL_ERR_IO);
+            if (b->u_send(b->u_io, b->tx, b->tx_used) == (int)b->tx_used) sent = b->tx_n;
+            else vb_fail(b, st = VAL_ERR_IO);
         } else {
-            for (uint32_t i = 0; i < b->tx_n && st == VAL_OK; i++) {
-                const size_t wl = (size_t)b->txf[i].len + VAL_WIRE_TRAILER_SIZE;
-                if (b->u_send(b->u_io, b->tx + b->txf[i].off, wl) != (int)wl) vb_fail(b, st = VAL_ERR_IO);
+            for (; sent < b->tx_n; sent++) {
+                const size_t wl = (size_t)b->txf[sent].len + VAL_WIRE_TRAILER_SIZE;
+                if (b->u_send(b->u_io, b->tx + b->txf[sent].off, wl) != (int)wl) {
+                    vb_fail(b, st = VAL_ERR_IO);
+                    break;
+                }
             }
         }
-        if (st == VAL_OK) b->st.tx_frames += b->tx_n;
     }
+    b->st.tx_frames += sent;
+    b->st.tx_unsent += b->tx_n - sent;
     b->tx_n = 0;
     b->tx_used = 0;
     return st;
+}
+
+/* A failure the session has not been told about (from transport.flush):
+ * reported by this call, once. */
+static int vb_take_err(val_batch_t *b)
+{
+    if (!b->err) return 0;
+    b->err = 0;
+    return 1;
 }
 
 static int vb_send(void *ctx, const void *data, size_t len)
@@ -220,19 +330,21 @@ static int vb_send(void *ctx, const void *data, size_t len)
     val_batch_t *b = (val_batch_t *)ctx;
     const size_t pending = b->tx_pending;
     b->tx_pending = 0;
-    if (b->st.status != VAL_OK) return -1;
-    /* the provider returned a placeholder for exactly this frame */
+    if (vb_take_err(b)) return -1;
+    /* the provider returned a placeholder for exactly this frame (and made
+       sure the window exists) */
     const int placeholder = data == (const void *)b->send_buffer && len >= VAL_WIRE_TRAILER_SIZE &&
-                            pending == len - VAL_WIRE_TRAILER_SIZE;
+                            pending == len - VAL_WIRE_TRAILER_SIZE && b->tx;
     if (!b->opt.tx || len < VAL_WIRE_HEADER_SIZE + VAL_WIRE_TRAILER_SIZE || len > b->opt.max_bytes ||
-        (!placeholder && b->tx_n == 0 && !vb_tx_engaged(b))) {
+        (!placeholder && b->tx_n == 0 && (!vb_tx_engaged(b) || !vb_tx_ready(b)))) {
         /* not a frame this batcher stages: send the window before it, then it */
         if (vb_flush_tx(b) != VAL_OK) return -1;
         const int rc = b->u_send(b->u_io, data, len);
         if (rc == (int)len) b->st.tx_frames++;
+        else vb_fail(b, VAL_ERR_IO);
         return rc;
     }
-    if (b->tx_n == b->opt.max_frames || b->tx_used + len > b->opt.max_bytes)
+    if (b->tx_n == b->opt.max_frames || b->tx_used + len > b->tx_cap)
         if (vb_flush_tx(b) != VAL_OK) return -1;
     vb_frame_t *f = &b->txf[b->tx_n++];
     f->off = b->tx_used;
@@ -250,7 +362,7 @@ static int vb_send(void *ctx, const void *data, size_t len)
 static void vb_flush_hook(void *ctx)
 {
     val_batch_t *b = (val_batch_t *)ctx;
-    (void)vb_flush_tx(b);
+    if (vb_flush_tx(b) != VAL_OK) b->err = 1;  /* flush has no status: the next send or recv reports it */
     if (b->u_flush) b->u_flush(b->u_io);
 }
 
@@ -276,24 +388,24 @@ static size_t vb_content_max(const val_batch_t *b)
     return b->mtu - VAL_WIRE_HEADER_SIZE - VAL_WIRE_TRAILER_SIZE;
 }
 
-/* Refill the empty ring: the frame in progress (or the next one), for which
- * the transport is given up to timeout_ms as the session would give it (over
- * as many partial reads as it takes), then, on a transport that polls
- * (recv_polls), every further byte it already holds (zero-timeout polls,
- * until one returns nothing). Complete frames that began in this ring are
- * hashed in one batch when this direction batches. Returns 0, or -1 on a
- * transport error. */
-static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
+/* Refill the empty ring. Batching (RX engaged, on a transport that polls,
+ * recv_polls): the frame in progress (or the next one), for which the
+ * transport is given up to timeout_ms as the session would give it (over as
+ * many partial reads as it takes), then every further byte it already holds
+ * (zero-timeout polls, until one returns nothing); the complete frames that
+ * began in this ring are hashed in one batch. Not batching: only until the
+ * `want` bytes the session asked for are in, so each of the session's reads
+ * waits no longer than it would on the bare transport (its header read does
+ * not wait for the content). Returns 0, or -1 on a transport error. */
+static int vb_fill(val_batch_t *b, uint32_t timeout_ms, size_t want)
 {
     b->r_base += b->r_len;
     b->r_head = b->r_len = 0;
     b->rx_n = b->rx_cur = 0;
-    const size_t cap = b->rx_cap;
-    if (b->raw) return 0;  /* passthrough: vb_recv reads what the session asks */
     const uint32_t t0 = b->ticks ? b->ticks() : 0u;
-    /* not batching now (or the transport cannot poll): the frame the session
-       asked for only, its check left to the provider */
-    const int eng = b->opt.recv_polls && vb_engaged(b, b->opt.rx);
+    int eng = b->opt.recv_polls && vb_engaged(b, b->opt.rx);
+    if (eng && !vb_rx_ready(b)) eng = 0;
+    const size_t cap = b->rx_cap;
     const uint32_t lim = eng ? b->opt.max_frames : 1u;
     uint32_t nread = 0;
     /* a frame carried over from the previous ring is delivered, not batched */
@@ -304,6 +416,7 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
         /* past the first frame every read is a zero-timeout poll: only on a
            transport that says it polls (val_batch_opts_t.recv_polls) */
         if (!first && !b->opt.recv_polls) break;
+        if (!eng && b->r_len >= want) break;
         uint32_t budget = 0;  /* frames read ahead: only what is there */
         if (first) {
             const uint32_t el = b->ticks ? b->ticks() - t0 : 0u;
@@ -330,18 +443,22 @@ static int vb_fill(val_batch_t *b, uint32_t timeout_ms)
             const size_t content = (size_t)b->hdr_part[2] | (size_t)b->hdr_part[3] << 8;
             if (content > vb_content_max(b)) {
                 /* the session will reject it (src/val_core.c:915-921); the
-                   stream has no trustworthy boundaries after this */
+                   stream has no trustworthy boundaries until it goes quiet */
                 b->raw = 1;
+                b->rs_seg = -1;
+                b->hdr_have = 0;
                 break;
             }
             b->cur_len = (uint32_t)(VAL_WIRE_HEADER_SIZE + content);
             b->owe = content + VAL_WIRE_TRAILER_SIZE;
+            if (!eng && b->r_len >= want) break;
         }
         const long r = vb_read(b, b->rx + b->r_len, b->owe, budget);
         if (r < 0) return -1;
         b->r_len += (size_t)r;
         b->owe -= (size_t)r;
         if (b->owe) {
+            if (!eng && b->r_len >= want) break;
             if (r > 0 && (!first || budget > 0)) continue;
             break;
         }
@@ -406,10 +523,53 @@ static void vb_track(val_batch_t *b, size_t pos, size_t n, const uint8_t *dst)
                 b->armed = 1;
                 b->armed_len = f->len;
                 b->armed_crc = f->crc;
+                /* f->len >= 8: every frame has its header */
+                memcpy(b->armed_head, b->rx + fs, VAL_WIRE_HEADER_SIZE);
+                b->armed_tail_n = f->len - VAL_WIRE_HEADER_SIZE < 8u ? f->len - VAL_WIRE_HEADER_SIZE : 8u;
+                memcpy(b->armed_tail, b->rx + fs + f->len - b->armed_tail_n, b->armed_tail_n);
             }
             b->rx_cur++;
             b->cur_matched = 0;
         }
+    }
+}
+
+/* Passthrough after an oversize header: follow the session's own reads. It
+ * reads a frame as header (8 bytes), then exactly the content its header
+ * announces, then the 4-byte trailer (src/val_core.c:893-945), over as many
+ * partial reads as the transport returns. Once its reads have taken one whole
+ * frame that way, this parser and the session agree where frames start
+ * again, and read-ahead resumes at the next frame. Reads of any other shape
+ * (a rejected header, a timeout mid-frame) restart the match at the session's
+ * next header read. */
+static void vb_raw_track(val_batch_t *b, const uint8_t *buf, size_t asked, size_t got)
+{
+    if (b->rs_seg < 0 || asked != b->rs_left) {
+        if (asked != VAL_WIRE_HEADER_SIZE) {
+            b->rs_seg = -1;
+            return;
+        }
+        b->rs_seg = 0;
+        b->rs_left = VAL_WIRE_HEADER_SIZE;
+    }
+    if (b->rs_seg == 0) memcpy(b->rs_hdr + (VAL_WIRE_HEADER_SIZE - b->rs_left), buf, got);
+    b->rs_left -= got;
+    if (b->rs_left) return;
+    if (b->rs_seg == 0) {
+        const size_t content = (size_t)b->rs_hdr[2] | (size_t)b->rs_hdr[3] << 8;
+        if (content > vb_content_max(b)) {
+            b->rs_seg = -1;
+            return;
+        }
+        b->rs_seg = content ? 1 : 2;
+        b->rs_left = content ? content : VAL_WIRE_TRAILER_SIZE;
+    } else if (b->rs_seg == 1) {
+        b->rs_seg = 2;
+        b->rs_left = VAL_WIRE_TRAILER_SIZE;
+    } else {  /* a whole frame as the session read it: the next byte starts a frame */
+        b->raw = 0;
+        b->owe = b->hdr_have = 0;
+        b->st.resyncs++;
     }
 }
 
@@ -418,15 +578,22 @@ static int vb_recv(void *ctx, void *buffer, size_t size, size_t *received, uint3
     val_batch_t *b = (val_batch_t *)ctx;
     if (received) *received = 0;
     if (size == 0) return 0;
-    /* the session is about to wait: its staged window goes out first */
+    if (vb_take_err(b)) return -1;
+    /* the session is about to wait: its staged window goes out first (a
+       failed send is this call's error: the session's ACK wait fails with
+       VAL_ERR_IO in the window whose frame was lost) */
     if (vb_flush_tx(b) != VAL_OK) return -1;
     if (!b->opt.rx) return b->u_recv(b->u_io, buffer, size, received, timeout_ms);
     if (b->r_head == b->r_len) {
         if (b->raw) {
             b->armed = 0;
-            return b->u_recv(b->u_io, buffer, size, received, timeout_ms);
+            size_t got = 0;
+            const int rc = b->u_recv(b->u_io, buffer, size, &got, timeout_ms);
+            if (received) *received = got;
+            if (rc >= 0) vb_raw_track(b, (const uint8_t *)buffer, size, got > size ? size : got);
+            return rc;
         }
-        if (vb_fill(b, timeout_ms) < 0) return -1;
+        if (vb_fill(b, timeout_ms, size) < 0) return -1;
     }
     size_t n = b->r_len - b->r_head;
     if (n > size) n = size;
@@ -440,6 +607,15 @@ static int vb_recv(void *ctx, void *buffer, size_t size, size_t *received, uint3
 }
 
 /* ---- the provider ------------------------------------------------------ */
+/* Whether the bytes at buf are the armed frame: its header and its last CRC-
+ * input bytes, which any other content put in recv_buffer since (a resume
+ * window read there, src/val_core.c:431-436, another frame) changes. */
+static int vb_arm_matches(const val_batch_t *b, const uint8_t *buf, size_t len)
+{
+    return memcmp(buf, b->armed_head, VAL_WIRE_HEADER_SIZE) == 0 &&
+           memcmp(buf + len - b->armed_tail_n, b->armed_tail, b->armed_tail_n) == 0;
+}
+
 uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
 {
     int rx = 0;
@@ -449,42 +625,43 @@ uint32_t val_batch_crc32_provider(uint32_t seed, const void *buf, size_t len)
            while batching: the trailer comes later from the window batch;
            control frames (ACK, DONE, ...) go out alone at once, so they are
            computed here */
-        if (seed == 0xFFFFFFFFu && len && ((const uint8_t *)buf)[0] == VAL_PKT_DATA && b->st.status == VAL_OK &&
-            vb_tx_engaged(b)) {
+        if (seed == 0xFFFFFFFFu && len && ((const uint8_t *)buf)[0] == VAL_PKT_DATA && vb_tx_engaged(b) &&
+            vb_tx_ready(b)) {
             b->tx_pending = len;
             return 0u;
         }
         return vb_direct(b, seed, buf, len);
     }
     if (b && b->armed && seed == 0xFFFFFFFFu && len == b->armed_len) {
-        b->armed = 0;
-        b->st.rx_batched_answers++;
-        return b->armed_crc;
+        if (vb_arm_matches(b, (const uint8_t *)buf, len)) {
+            b->armed = 0;
+            b->st.rx_batched_answers++;
+            return b->armed_crc;
+        }
+        b->st.arm_rejects++;  /* recv_buffer no longer holds the armed frame: computed directly */
     }
     return vb_direct(b, seed, buf, len);
 }
 
 /* ---- lifetime ---------------------------------------------------------- */
-static void *vb_alloc(const val_batch_t *b, size_t n, int *pinned)
-{
-    void *p = b->pinned ? val_gpu_host_alloc(n) : NULL;
-    *pinned = p != NULL;
-    return p ? p : malloc(n);
-}
-
-static void vb_free(void *p, int pinned)
-{
-    if (!p) return;
-    if (pinned) val_gpu_host_free(p);
-    else free(p);
-}
-
 /* buffers first, so no lookup matches a slot whose batcher is going */
 static void vb_release_slot(int i)
 {
     __atomic_store_n(&g_buf[0][i], NULL, __ATOMIC_RELEASE);
     __atomic_store_n(&g_buf[1][i], NULL, __ATOMIC_RELEASE);
     __atomic_store_n(&g_reg[i], NULL, __ATOMIC_RELEASE);
+}
+
+static void vb_destroy(val_batch_t *b)
+{
+    vb_free(b->tx, b->tx_pinned);
+    vb_free(b->rx, b->rx_pinned);
+    free(b->txf);
+    free(b->rxf);
+    free(b->crc_tmp);
+    free(b->off_tmp);
+    free(b->len_tmp);
+    free(b);
 }
 
 val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, val_batch_t **out)
@@ -519,10 +696,6 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
                                                     : w > VB_MAX_DEFAULT_BYTES ? VB_MAX_DEFAULT_BYTES : (size_t)w;
     }
     if (b->opt.max_bytes < b->mtu) b->opt.max_bytes = b->mtu;
-    /* buffers only where they can be used: no TX window without TX batching,
-       an RX ring of one frame without read-ahead */
-    const size_t tx_cap = b->opt.tx ? b->opt.max_bytes : 16u;
-    b->rx_cap = (b->opt.rx && b->opt.recv_polls) ? b->opt.max_bytes : b->mtu;
     b->cfg = cfg;
     b->u_send = cfg->transport.send;
     b->u_recv = cfg->transport.recv;
@@ -533,38 +706,29 @@ val_status_t val_batch_attach(val_config_t *cfg, const val_batch_opts_t *opts, v
     b->ticks = cfg->system.get_ticks_ms;
     b->send_buffer = (const uint8_t *)cfg->buffers.send_buffer;
     b->recv_buffer = (const uint8_t *)cfg->buffers.recv_buffer;
-    b->pinned = val_gpu_device_count() > 0;  /* pinned windows: DMA in place on the GPU path */
-    const uint32_t nf = b->opt.max_frames;
-    b->tx = (uint8_t *)vb_alloc(b, tx_cap, &b->tx_pinned);
-    b->rx = (uint8_t *)vb_alloc(b, b->rx_cap, &b->rx_pinned);
-    b->txf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
-    b->rxf = (vb_frame_t *)calloc(nf, sizeof(vb_frame_t));
-    b->crc_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
-    b->off_tmp = (uint64_t *)calloc(nf, sizeof(uint64_t));
-    b->len_tmp = (uint32_t *)calloc(nf, sizeof(uint32_t));
+    /* pinned windows (DMA in place on the GPU path) when a device is present;
+       a batcher with both directions off never starts the HIP runtime */
+    b->pinned = (b->opt.tx || b->opt.rx) && val_gpu_device_count() > 0;
+    /* the RX ring holds one frame until RX first batches; the TX window and
+       the per-frame arrays come with the first batch (vb_tx_ready,
+       vb_rx_ready): a session whose windows never reach the crossover
+       allocates no window */
+    b->rx_cap = b->mtu;
+    b->rx = (uint8_t *)malloc(b->rx_cap);
     int slot = -1;
-    for (int i = 0; i < VB_MAX_ATTACHED && slot < 0; i++) {
+    for (int i = 0; i < VB_MAX_ATTACHED && slot < 0 && b->rx; i++) {
         val_batch_t *expect = NULL;
         if (__atomic_compare_exchange_n(&g_reg[i], &expect, b, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) slot = i;
     }
-    if (slot >= 0) {
-        __atomic_store_n(&g_buf[0][slot], (const void *)b->send_buffer, __ATOMIC_RELEASE);
-        __atomic_store_n(&g_buf[1][slot], (const void *)b->recv_buffer, __ATOMIC_RELEASE);
-        int h = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
-        while (h < slot + 1 && !__atomic_compare_exchange_n(&g_hwm, &h, slot + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-        }
+    if (!b->rx || slot < 0) {
+        const val_status_t st = b->rx ? VAL_ERR_INVALID_ARG : VAL_ERR_NO_MEMORY;
+        vb_destroy(b);
+        return st;
     }
-    if (!b->tx || !b->rx || !b->txf || !b->rxf || !b->crc_tmp || !b->off_tmp || !b->len_tmp || slot < 0) {
-        if (slot >= 0) vb_release_slot(slot);
-        vb_free(b->tx, b->tx_pinned);
-        vb_free(b->rx, b->rx_pinned);
-        free(b->txf);
-        free(b->rxf);
-        free(b->crc_tmp);
-        free(b->off_tmp);
-        free(b->len_tmp);
-        free(b);
-        return slot < 0 ? VAL_ERR_INVALID_ARG : VAL_ERR_NO_MEMORY;
+    __atomic_store_n(&g_buf[0][slot], (const void *)b->send_buffer, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_buf[1][slot], (const void *)b->recv_buffer, __ATOMIC_RELEASE);
+    int h = __atomic_load_n(&g_hwm, __ATOMIC_ACQUIRE);
+    while (h < slot + 1 && !__atomic_compare_exchange_n(&g_hwm, &h, slot + 1, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
     }
     b->st.status = VAL_OK;
     cfg->transport.send = vb_send;
@@ -608,12 +772,5 @@ void val_batch_detach(val_batch_t *b)
     cfg->transport.flush = b->u_flush;
     cfg->transport.io_context = b->u_io;
     cfg->crc32_provider = b->u_provider;
-    vb_free(b->tx, b->tx_pinned);
-    vb_free(b->rx, b->rx_pinned);
-    free(b->txf);
-    free(b->rxf);
-    free(b->crc_tmp);
-    free(b->off_tmp);
-    free(b->len_tmp);
-    free(b);
+    vb_destroy(b);
 }

@@ -1500,14 +1500,43 @@ void shard_frames(uint32_t n, const uint32_t *len, uint32_t world, uint32_t rank
 // C1 (host_batch_min_bytes) was measured against one CPU thread. With N
 // devices each shard's H2D runs on its own PCIe link and DMA engines while
 // the fixed costs (launch, completion wait, first chunk) are paid
-// concurrently, so the GPU side's byte rate scales with N; the CPU engine's
-// scales with its T threads (val_gpu_set_host_cpu_threads, capped by the
-// CPU budget). First-order crossover: C(N, T) = C1 * T / N (DESIGN.md
-// section 1). A GPU test that forces C1 = 0 keeps every batch on the GPU.
-uint64_t host_multi_min_bytes(int devices, uint64_t mean_len = UINT64_MAX)
+// concurrently, so for pinned input the GPU side's byte rate scales with N;
+// the CPU engine's scales with its T threads (val_gpu_set_host_cpu_threads,
+// capped by the CPU budget): C(N, T) = C1 * T / N.
+// Pageable input also passes through the host bounce copies, which all
+// shards share inside the process's CPU budget. Measured on the GPU box
+// (16 CPUs, tools/bounce_copy_scaling.py, profiles/r06_bounce_copy_scaling.
+// jsonl): one copy thread moves about 14 GB/s and all copies together
+// saturate near 135 GB/s (112 / 124 / 151 / 136 GB/s at 1 / 2 / 4 / 8
+// concurrent 64 MiB copies), while one GPU's pageable host path takes about
+// 53 GB/s. So N pageable shards feed at most N_eff = min(N, R_copy(N) / 53)
+// devices' worth of GPU (2.55 at N >= 4 on the box), and C(N, T) = C1 * T /
+// N_eff. A GPU test that forces C1 = 0 keeps every batch on the GPU.
+#ifndef VCRC_COPY_MBS_PER_THREAD
+#define VCRC_COPY_MBS_PER_THREAD 14000u  // MB/s one bounce-copy thread moves
+#endif
+#ifndef VCRC_COPY_MBS_MAX
+#define VCRC_COPY_MBS_MAX 135000u  // MB/s all bounce copies of the process together
+#endif
+#ifndef VCRC_PAGEABLE_MBS_PER_GPU
+#define VCRC_PAGEABLE_MBS_PER_GPU 53000u  // MB/s of one GPU's pageable host path (49.6 GiB/s)
+#endif
+
+// N_eff * 16 for `devices` shards (pinned: N * 16).
+uint64_t host_multi_devices_x16(int devices, bool pinned)
+{
+    const uint64_t n = (uint64_t)std::max(1, devices);
+    if (pinned) return n * 16u;
+    const uint64_t threads =
+        std::min<uint64_t>(host_cpu_budget(), n * copy_threads(host_chunk_bytes(), (uint32_t)n));
+    const uint64_t copy = std::min<uint64_t>(threads * VCRC_COPY_MBS_PER_THREAD, VCRC_COPY_MBS_MAX);
+    return std::max<uint64_t>(16u, std::min<uint64_t>(n * 16u, copy * 16u / VCRC_PAGEABLE_MBS_PER_GPU));
+}
+
+uint64_t host_multi_min_bytes(int devices, uint64_t mean_len = UINT64_MAX, bool pinned = false)
 {
     const uint64_t t = std::max<uint64_t>(1, std::min<uint64_t>(g_host_cpu_threads.load(), host_cpu_budget()));
-    return host_batch_min_bytes(mean_len) * t / (uint64_t)std::max(1, devices);
+    return host_batch_min_bytes(mean_len) * t * 16u / host_multi_devices_x16(devices, pinned);
 }
 
 // Run work(0..k-1): k-1 helper threads plus the calling thread; a helper that
@@ -1551,7 +1580,8 @@ val_status_t frames_host_multi(const uint8_t *base, uint64_t base_len, const uin
     if (ndev <= 0) ndev = std::max(1, std::min(count, kMaxDevices));
     ndev = std::min(ndev, kMaxDevices);
     // one decision for the whole batch: distinct devices the shards land on
-    if (total < host_multi_min_bytes(std::max(1, std::min(ndev, count)), n ? total / n : 0)) {
+    if (total < host_multi_min_bytes(std::max(1, std::min(ndev, count)), n ? total / n : 0,
+                                 n && count > 0 && is_pinned(base))) {
         const uint32_t bad = cpu_frames(base, off, len, stride, flen, n, total, verify, crc, hdr, ok, nullptr);
         if (nbad) *nbad = verify ? bad : 0u;
         return VAL_OK;
@@ -1602,7 +1632,8 @@ val_status_t region_host_multi(const void *data, uint64_t len, uint32_t state_in
     }
     if (ndev <= 0) ndev = std::max(1, std::min(count, kMaxDevices));
     ndev = std::min(ndev, kMaxDevices);
-    const bool on_cpu = len < host_multi_min_bytes(std::max(1, std::min(ndev, count)));
+    const bool on_cpu =
+        len < host_multi_min_bytes(std::max(1, std::min(ndev, count)), UINT64_MAX, len && count > 0 && is_pinned(data));
     if (!on_cpu && count <= 0) return fail(VAL_ERR_IO, "no HIP device");
     int parts = ndev;
     if (on_cpu) {
@@ -1859,6 +1890,8 @@ void val_gpu_set_host_batch_min_bytes(int64_t bytes) { g_host_batch_min.store(by
 
 uint64_t val_gpu_host_batch_min_bytes(void) { return host_batch_min_bytes(); }
 
+uint64_t val_gpu_host_batch_min_bytes_for(uint64_t mean_len) { return host_batch_min_bytes(mean_len); }
+
 uint64_t val_gpu_cpu_batch_count(void) { return g_cpu_batches.load(std::memory_order_relaxed); }
 
 void val_gpu_set_host_cpu_threads(uint32_t threads)
@@ -1867,6 +1900,11 @@ void val_gpu_set_host_cpu_threads(uint32_t threads)
 }
 
 uint64_t val_gpu_host_multi_min_bytes(int devices) { return host_multi_min_bytes(devices); }
+
+uint64_t val_gpu_host_multi_min_bytes_ex(int devices, int pinned, uint64_t mean_len)
+{
+    return host_multi_min_bytes(devices, mean_len, pinned != 0);
+}
 
 void val_gpu_set_ragged_min_frames(int64_t frames) { g_ragged_min.store(frames < 0 ? -1 : frames); }
 
@@ -1898,6 +1936,63 @@ int val_crc32_cpu_engine(void) { return vcrc_cpu_engine(); }
 uint32_t val_gpu_host_copy_threads(uint64_t bytes, uint32_t concurrent_copies)
 {
     return copy_threads(bytes, concurrent_copies);
+}
+
+val_status_t val_gpu_host_copy_probe(uint32_t copies, uint64_t bytes, uint32_t reps, int pinned_dst, double *gbs)
+{
+    if (!copies || copies > 64 || !bytes || !reps || !gbs) return fail(VAL_ERR_INVALID_ARG, "copy probe arguments");
+    *gbs = 0.0;
+    std::vector<uint8_t *> src(copies, nullptr), dst(copies, nullptr);
+    val_status_t st = VAL_OK;
+    for (uint32_t i = 0; i < copies && st == VAL_OK; i++) {
+        src[i] = static_cast<uint8_t *>(malloc(bytes));
+        if (!src[i]) {
+            st = fail(VAL_ERR_NO_MEMORY, "copy probe: source");
+            break;
+        }
+        memset(src[i], (int)(i + 1), bytes);  // resident, like a transport's window
+        if (pinned_dst) {
+            const hipError_t e = hipHostMalloc((void **)&dst[i], bytes, hipHostMallocDefault);
+            if (e != hipSuccess) {
+                dst[i] = nullptr;
+                st = fail(VAL_ERR_IO, "copy probe: hipHostMalloc", e);
+            }
+        } else if (!(dst[i] = static_cast<uint8_t *>(malloc(bytes)))) {
+            st = fail(VAL_ERR_NO_MEMORY, "copy probe: destination");
+        }
+        if (dst[i]) memset(dst[i], 0, bytes);
+    }
+    if (st == VAL_OK) {
+        // every copy stream starts together; the span is first start to last end
+        std::atomic<uint32_t> ready{0};
+        std::atomic<bool> go{false};
+        auto work = [&](int i) {
+            ready.fetch_add(1);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            for (uint32_t r = 0; r < reps; r++) parallel_copy(dst[i], src[i], bytes);
+        };
+        std::vector<std::thread> th;
+        try {
+            for (uint32_t i = 1; i < copies; i++) th.emplace_back(work, (int)i);
+        } catch (...) {
+            st = fail(VAL_ERR_NO_MEMORY, "copy probe: thread");
+        }
+        while (ready.load() < (uint32_t)th.size()) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        go.store(true, std::memory_order_release);
+        if (st == VAL_OK) work(0);
+        for (auto &x : th) x.join();
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (st == VAL_OK) *gbs = (double)bytes * reps * copies / s / 1e9;
+    }
+    for (uint32_t i = 0; i < copies; i++) {
+        free(src[i]);
+        if (dst[i]) {
+            if (pinned_dst) (void)hipHostFree(dst[i]);
+            else free(dst[i]);
+        }
+    }
+    return st;
 }
 
 uint64_t val_gpu_cpu_fallback_count(void) { return g_cpu_fallbacks.load(std::memory_order_relaxed); }
