@@ -601,3 +601,41 @@ def test_oversize_header_then_a_transfer_reads_ahead_again(gpu):
                 assert rx["rx_batched_answers"] >= 1000, rx
     finally:
         os.environ.pop("VAL_HARNESS_MAX_TIMEOUT_MS", None)
+
+
+def test_auto_threshold_follows_the_frame_size():
+    """AUTO decides with the crossover for the session's frames:
+    val_gpu_host_batch_min_bytes_for(mean CRC input), the threshold
+    val_crc32_frames_host applies to the batch it would send: 32 MiB below a
+    4 KiB mean, 64 MiB from 4 KiB. The built-in
+    values, in a process without the suite's forced thresholds."""
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("VAL_GPU_HOST_BATCH_MIN_BYTES", "VAL_GPU_PROVIDER_MIN_BYTES")}
+    code = ("import sys; sys.path.insert(0, %r); import val_protocol_amd.crc as vc; l = vc.lib(); "
+            "print([l.val_gpu_host_batch_min_bytes_for(m) for m in (1020, 4095, 4096, 65532)], "
+            "l.val_gpu_host_batch_min_bytes())") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == str([32 << 20, 32 << 20, 64 << 20, 64 << 20]) + " " + str(64 << 20)
+
+
+@needs_harness
+@pytest.mark.gpu
+def test_auto_engages_at_the_short_frame_crossover():
+    """On the GPU at the library's built-in thresholds: an MTU-1,024 session
+    whose window is 40,000 frames (41 MB, between the 32 MiB short-frame
+    crossover and the 64 MiB one) batches in AUTO mode, as its batches would
+    run on the GPU; before round 6 AUTO compared it with 64 MiB and passed
+    every frame through."""
+    os.environ["VAL_HARNESS_BATCH_MODE"] = "auto"
+    try:  # gpu=False: the harness runs without the suite's forced thresholds (the built-in ones)
+        got = _line(_run([vc.LIB_PATH, "loopback-batched", 48 << 20, 1024, 40000], False, timeout=400))
+    finally:
+        os.environ.pop("VAL_HARNESS_BATCH_MODE", None)
+    assert got["tx_status"] == VAL_OK and got["rx_status"] == VAL_OK and got["equal"] == 1, got
+    assert got["rx_crc_errors"] == 0 and got["trailers_ok"] == got["wire_frames"]
+    tx, rx = got["batch"]
+    assert tx["tx_batches"] >= 1 and tx["tx_max_batch"] >= 30000, tx
+    assert rx["rx_batched_answers"] > 0, rx
