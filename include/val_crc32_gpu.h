@@ -281,6 +281,15 @@ uint32_t val_gpu_host_copy_threads(uint64_t bytes, uint32_t concurrent_copies);
  * copy's end, in GB/s. DESIGN.md section 1.3 folds it into the N-device
  * crossover. */
 val_status_t val_gpu_host_copy_probe(uint32_t copies, uint64_t bytes, uint32_t reps, int pinned_dst, double *gbs);
+/* Uniform batches whose frame groups do not fill the last round of the
+ * persistent grid (e.g. 131,113 x 64 KiB frames: 8 rounds and 41 frames)
+ * hash the frames past the last full round in pieces inside the same
+ * launch (1-4 KiB pieces; 8 or 16 lanes per frame, frames of 8 KiB and more), instead of a
+ * second launch. 1 / 0 switch it on / off, -1 = VAL_GPU_TAIL_PIECES (unset:
+ * on). Speed only; results never change. _launches counts the launches that
+ * used it. */
+void val_gpu_set_tail_pieces(int enable);
+uint64_t val_gpu_tail_piece_launches(void);
 /* Wire bytes per H2D chunk of the *_frames_host calls; 0 = default (64 MiB).
  * Device memory use is two chunks. Speed and memory only; results never change. */
 val_status_t val_gpu_set_host_chunk_bytes(size_t bytes);

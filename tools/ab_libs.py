@@ -47,6 +47,13 @@ def workload(name, dev):
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         off = torch.arange(n, device=dev, dtype=torch.int64) * (L + 4)
         return dict(buf=buf, off=off, length=torch.full((n,), L, dtype=torch.int32, device=dev), len_hint=L), n * L
+    if name.startswith("t") and name[1:].isdigit():  # tNNNNN: a cfg4 slice, NNNNN x 65,532 B, the last 816 B,
+        n, L = int(name[1:]), 65532                    # descriptors with the uniform hint (bench.py's slices)
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        off = torch.arange(n, device=dev, dtype=torch.int64) * (L + 4)
+        length = torch.full((n,), L, dtype=torch.int32, device=dev)
+        length[-1] = 816
+        return dict(buf=buf, off=off, length=length, len_hint=L), int(length.long().sum().item())
     if name in ("cfg3", "cfg3b"):  # cfg3b: the bench layout (flen 16400, stride 16404)
         n, L = 1 << 20, (16384 - 4 if name == "cfg3" else 16400)
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

@@ -58,6 +58,7 @@ EXPORTS = (
     "val_gpu_scratch_entries", "val_gpu_set_host_batch_min_bytes", "val_gpu_host_batch_min_bytes",
     "val_gpu_host_batch_min_bytes_for",
     "val_gpu_cpu_batch_count", "val_gpu_set_host_cpu_threads", "val_gpu_host_multi_min_bytes", "val_gpu_host_multi_min_bytes_ex",
+    "val_gpu_set_tail_pieces", "val_gpu_tail_piece_launches",
     "val_batch_attach", "val_batch_flush", "val_batch_get_stats", "val_batch_detach", "val_batch_crc32_provider",
     "val_serialize_handshake", "val_deserialize_handshake", "val_serialize_meta", "val_deserialize_meta",
     "val_serialize_resume_resp", "val_deserialize_resume_resp", "val_serialize_verify_request",
@@ -159,6 +160,8 @@ def _declare(lib: ctypes.CDLL, strict: bool = True) -> None:
     fn("val_gpu_set_host_cpu_threads", None, u32)
     fn("val_gpu_host_multi_min_bytes", u64, ctypes.c_int)
     fn("val_gpu_host_multi_min_bytes_ex", u64, ctypes.c_int, ctypes.c_int, u64)
+    fn("val_gpu_set_tail_pieces", None, ctypes.c_int)
+    fn("val_gpu_tail_piece_launches", u64)
 
 
 def lib() -> ctypes.CDLL:

@@ -132,11 +132,17 @@ __host__ __device__ constexpr uint32_t pow_map(int k) { return kLdsPow + (uint32
 //   [kConstTree,  +6*128)  nibble map "advance 64 * 2^j bytes" (merge level j)
 //   [kConstPow,  +48*128)  nibble map "advance 2^k bytes", k = 0..47
 //   [kConstPowHi,    +16)  x^(8 * 2^k) mod P for k = 16..31 (shifts past 64 KiB, VALU)
+//   [kConstXpow,     +48)  x^(8 * 2^k) mod P for k = 0..47 (VALU shifts by any distance)
+//   [kConstPieceMul, +4*128) x^(8 * j * 2^k0) mod P for k0 = 10..13, j = 0..127: one VALU
+//                          product per piece for k_frames' in-launch tail pieces
 // The maps are contiguous, in LDS order.
 constexpr uint32_t kConstSlice = 0, kConstGap = 1024, kConstTree = 1024 + 7 * 128;
 constexpr uint32_t kConstPow = kConstTree + kMaxTree * 128;
 constexpr uint32_t kConstPowHi = kConstPow + kBlobPowMaps * 128;
-constexpr uint32_t kConstWords = kConstPowHi + 16;
+constexpr uint32_t kConstXpow = kConstPowHi + 16;
+constexpr uint32_t kPieceK0Min = 10, kPieceK0Max = 13, kPieceMulJ = 128;
+constexpr uint32_t kConstPieceMul = kConstXpow + 48;
+constexpr uint32_t kConstWords = kConstPieceMul + (kPieceK0Max - kPieceK0Min + 1) * kPieceMulJ;
 
 // Prologue: the slice tables are written in 16-B chunks, chunk c = r * 1024 + t
 // for thread t, so the 64 lanes of a ds_write_b128 fill 1 KiB contiguously
@@ -259,6 +265,23 @@ __host__ inline void fill_const_blob(uint32_t *w)
         for (int t = 0; t < 128; t++) w[kConstPow + k * 128 + t] = gf2_mul(x, (uint32_t)(t & 15) << (4 * (t >> 4)));
     }
     for (int k = 16; k < 32; k++) w[kConstPowHi + k - 16] = gf2_x8n((uint64_t)1 << k);
+    for (int k = 0; k < 48; k++) w[kConstXpow + k] = gf2_x8n((uint64_t)1 << k);
+    for (uint32_t k0 = kPieceK0Min; k0 <= kPieceK0Max; k0++)
+        for (uint32_t j = 0; j < kPieceMulJ; j++)
+            w[kConstPieceMul + (k0 - kPieceK0Min) * kPieceMulJ + j] = gf2_x8n((uint64_t)j << k0);
+}
+
+// Advance raw register v over n zero bytes with VALU multiplies only (one
+// GF(2) product per set bit of n, constants from the blob): no LDS maps, for
+// the rare shifts of launches that do not fill the pow slots.
+__device__ __forceinline__ uint32_t shift_bytes_valu(uint32_t v, uint64_t n, const uint32_t *consts)
+{
+    while (n) {
+        const int k = __builtin_ctzll(n);
+        v = gf2_mul(consts[kConstXpow + (uint32_t)k], v);
+        n &= n - 1;
+    }
+    return v;
 }
 
 __host__ __device__ constexpr int ilog2(int g) { return g <= 1 ? 0 : 1 + ilog2(g >> 1); }

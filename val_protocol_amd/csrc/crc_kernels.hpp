@@ -77,6 +77,12 @@ struct FrameParams {
     uint32_t *qhead;         // uniform mode: dynamic-tail queue, kDynQueueBytes (zero on entry, re-zeroed), nullable
     uint32_t static_rounds;  // with qhead: group rounds dealt statically before the queue
     uint32_t qparts;         // with qhead: queue partitions, 1..kDynParts
+    // uniform mode, G >= 8: frames [n, n + tail_n) hashed in pieces inside this launch (tail_pieces)
+    uint32_t tail_n;         // 0: none
+    uint32_t tail_units;     // pieces per tail frame
+    uint32_t tail_k0;        // piece bytes W = 2^tail_k0
+    uint32_t tail_last_len;  // strided mode: length of the last tail frame
+    uint32_t *tail_acc;      // {register, arrivals} per tail frame (zero on entry, re-zeroed)
 };
 
 // Bytes before a DATA frame's payload: the 8-B header, plus the 8-B file
@@ -623,6 +629,100 @@ __device__ __forceinline__ void group_pass(const FrameParams &p, uint64_t &f, ui
     fb += step;
 }
 
+// In-launch tail of a uniform launch (launch_uniform). A batch whose frame
+// groups do not fill the last wave-round (131,113 x 64 KiB frames: 8 rounds
+// and 41 frames; a 1 GiB eighth of that file: one round and 6 frames) used to
+// hash those frames in a second small launch after this one: a launch boundary
+// and a 12-14 us latency-bound kernel on 6-41 CUs, 9% of a 1 GiB step. Here
+// they are cut into pieces that the waves hash as one extra frame group each,
+// after their own groups, the oldest waves first (a SIMD's oldest waves
+// finish first, see above): piece j of a tail frame of L bytes covers
+// [L - (j+1) W, L - j W) (W = 2^tail_k0, 1 KiB unless the pieces would need
+// more groups than there are waves), the front piece everything before
+// it, and the piece holding the frame's first byte carries the seed. Each
+// piece's register is advanced over the j W bytes after it and XORed into the
+// frame's accumulator (device-scope atomics, each returned before the next is
+// issued, as k_region folds); the frame's last piece to count in writes its
+// outputs (trailer CRC, header_crc, verify) and re-zeroes the accumulator.
+__device__ __forceinline__ void tail_desc(const FrameParams &p, uint32_t t, uint64_t &off, uint32_t &L)
+{
+    const uint64_t f = (uint64_t)p.n + t;
+    if (p.off) {
+        off = p.off[f];
+        L = p.len[f];
+    } else {
+        const uint32_t flen = p.flen, last = p.tail_last_len;
+        off = f * p.stride;
+        L = (t + 1 == p.tail_n) ? last : flen;
+    }
+}
+
+// Instances that carry the path: 8 and 16 lanes per frame (2-48 KiB and longer
+// frames), the default round depth; in the others its registers made the
+// 32- and 64-lane one-pass kernels spill.
+template <int G, int PF, bool PAY, int BT>
+constexpr bool kTailPieces = (G == 8 || G == 16) && PF == 1 && !PAY && BT == kBlock;
+
+template <int G, int PF, bool C0>
+__device__ __forceinline__ void tail_pieces(const FrameParams &p, int lane, const SliceBases &sb)
+{
+    constexpr int kGroups = 64 / G;
+    const uint32_t total = p.tail_n * p.tail_units;
+    const uint32_t wg = (uint32_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;  // oldest waves first
+    if (wg * (uint32_t)kGroups >= total) return;                                // wave-uniform
+    const uint32_t u = wg * (uint32_t)kGroups + (uint32_t)(lane / G);
+    const bool real = u < total;
+    const uint32_t t = real ? u / p.tail_units : 0u, j = real ? u % p.tail_units : 0u;
+    uint64_t off = 0;
+    uint32_t L = 0;
+    if (real) tail_desc(p, t, off, L);
+    const uint64_t after = (uint64_t)j << p.tail_k0;  // bytes of the frame after this piece
+    const uint32_t W = 1u << p.tail_k0;
+    const uint32_t hi = (uint64_t)L > after ? (uint32_t)((uint64_t)L - after) : 0u;
+    const uint32_t lo = (j + 1u == p.tail_units || hi <= W) ? 0u : hi - W;
+    const bool carrier = real && lo == 0u && (hi > 0u || j == 0u);  // holds byte 0 (or is an empty frame's piece 0)
+    const bool act = real && (hi > lo || carrier);
+    FrameParams q{};
+    q.base = p.base;
+    q.consts = p.consts;
+    q.seed0 = p.seed_rest;  // a tail frame is never frame 0 of the batch
+    const uint32_t st = hash_frame<G, PF, false, false, C0>(q, carrier ? 0u : 1u, act, off + lo, act ? hi - lo : 0u,
+                                                         lane % G, sb, G, [] {});
+    if (!real || lane % G != G - 1) return;
+    uint32_t v = 0;
+    if (act) {  // one product from the blob's piece table (any other distance: a product per set bit)
+        const bool tab = p.tail_k0 >= kPieceK0Min && p.tail_k0 <= kPieceK0Max && j < kPieceMulJ;
+        v = tab ? gf2_mul(p.consts[kConstPieceMul + (p.tail_k0 - kPieceK0Min) * kPieceMulJ + j], st)
+                : shift_bytes_valu(st, after, p.consts);
+    }
+    uint32_t *a = p.tail_acc + 2u * t;
+    const uint32_t old = atomicXor(&a[0], v);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
+    const uint32_t arrived = atomicAdd(&a[1], 1u);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(arrived) : "memory");
+    if (arrived + 1u != p.tail_units) return;
+    const uint32_t crc = atomicExch(&a[0], 0u) ^ p.xorout;
+    atomicExch(&a[1], 0u);
+    const uint64_t f = (uint64_t)p.n + t;
+    gu8 *fp = gptr(p.base) + off;
+    if (p.out_crc) p.out_crc[f] = crc;
+    if (p.out_hdr) {
+        uint32_t h = p.seed_rest;
+        if (L >= 8) {
+            h = s4_step(h, ld32(fp), sb);
+            h = s4_step(h, ld32(fp + 4), sb);
+        } else {
+            for (uint32_t i = 0; i < L; i++) h = byte_step(h, fp[i], sb);
+        }
+        p.out_hdr[f] = h ^ p.xorout;
+    }
+    if (p.verify) {
+        const bool good = crc == ld32(fp + L);
+        if (p.out_ok) p.out_ok[f] = good ? 1u : 0u;
+        if (!good && p.nbad) atomicAdd(p.nbad, 1u);
+    }
+}
+
 // BT: threads per workgroup. 1,024 (16 waves, 128 VGPRs) everywhere, or 512
 // (8 waves, up to 256 VGPRs: deeper rings for short frames; an A/B that lost
 // 10-24%, val_crc32_hip.hip VCRC_W8_PF).
@@ -665,6 +765,9 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
     });
     if (!p.qhead) {
         while (fb < p.n) group_pass<G, PF, PAY, C0>(p, f, off, L, fb, nwaves * kGroups, lane, sb, [] {});
+        if constexpr (kTailPieces<G, PF, PAY, BT>) {
+            if (p.tail_n) tail_pieces<G, PF, C0>(p, lane, sb);
+        }
         VCRC_STAMP(2);
         return;
     }
@@ -729,6 +832,9 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
         fd = fd_n;
         od = od_n;
         Ld = Ld_n;
+    }
+    if constexpr (kTailPieces<G, PF, PAY, BT>) {
+        if (p.tail_n) tail_pieces<G, PF, C0>(p, ql, sb);
     }
     VCRC_STAMP(2);
     if (ql == 0) {

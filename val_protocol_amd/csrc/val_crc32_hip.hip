@@ -68,6 +68,7 @@ struct StreamScratch {
     Arena region;  // k_region accumulator + arrival count (128 B, zero between calls)
     Arena bin;     // ragged binning: counts, plan, sorted order
     Arena queue;   // k_frames dynamic tail {head, exits} (zero between calls)
+    Arena tail;    // k_frames in-launch tail pieces: {register, arrivals} per tail frame (zero between calls)
 };
 // Streams with scratch per device; beyond this the least recently used entry
 // is evicted (a program that keeps creating streams would otherwise grow the
@@ -478,8 +479,19 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     Ctx &cm = const_cast<Ctx &>(c);
     std::lock_guard<std::recursive_mutex> lk(cm.mu);
     StreamScratch *used = nullptr;
-    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
+    if (p.tail_n) {  // in-launch tail pieces (launch_uniform): a zeroed accumulator pair per tail frame
         used = &scratch_for(cm, s);
+        Arena &a = used->tail;
+        uint8_t *q = nullptr;
+        const size_t bytes = (size_t)p.tail_n * 8u;
+        val_status_t st = arena_acquire(a, bytes, s, &q);
+        if (st != VAL_OK) return st;
+        if (!a.counts_zero) VCRC_HIP(hipMemsetAsync(q, 0, a.cap, s), "hipMemsetAsync(tail)");
+        a.counts_zero = false;  // set again once the launch is queued (its last pieces re-zero the pairs)
+        p.tail_acc = reinterpret_cast<uint32_t *>(q);
+    }
+    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
+        if (!used) used = &scratch_for(cm, s);
         Arena &a = used->queue;
         uint8_t *q = nullptr;
         val_status_t st = arena_acquire(a, kDynQueueBytes, s, &q);
@@ -511,8 +523,40 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     case 64: e = launch_uniform_g<64>(pf, grid, s, p, one_pass, used, len); break;
     default: return fail(VAL_ERR_INVALID_ARG, "bad lanes-per-frame");
     }
+    if (p.tail_n && e == hipSuccess) used->tail.counts_zero = true;
     VCRC_HIP(e, "k_frames launch");
     return VAL_OK;
+}
+
+// In-launch tail pieces (crc_kernels.hpp tail_pieces): the frames past the
+// last full wave-round, cut into pieces of W = 2^k0 bytes and hashed by the
+// oldest waves as one extra frame group each, instead of a second launch.
+// W = 1 KiB (one round at 16 lanes: the extra work per wave stays under what
+// the oldest waves gain on the youngest), doubled while the piece groups
+// outnumber the waves. Kernels with G = 8 or 16 at the default depth carry
+// the path; frames of at least 8 KiB use it. VAL_GPU_TAIL_PIECES=0 or
+// val_gpu_set_tail_pieces(0) keeps the second launch (A/B).
+std::atomic<int> g_tail_pieces{-1};  // -1: VAL_GPU_TAIL_PIECES (unset = on); 0 / 1: val_gpu_set_tail_pieces
+std::atomic<uint64_t> g_tail_piece_launches{0};
+bool tail_pieces_enabled()
+{
+    const int v = g_tail_pieces.load(std::memory_order_relaxed);
+    if (v >= 0) return v != 0;
+    static const bool on = !(getenv("VAL_GPU_TAIL_PIECES") && atoi(getenv("VAL_GPU_TAIL_PIECES")) == 0);
+    return on;
+}
+
+// log2 of the piece bytes for this tail, or 0 when the path does not apply.
+uint32_t tail_piece_k0(const Ctx &c, const FrameParams &p, uint32_t G, uint32_t len, uint64_t n_tail)
+{
+    if (!tail_pieces_enabled() || p.out_pay || (G != 8 && G != 16) || len < 8192u || n_tail == 0 ||
+        forced_prefetch() != -1)
+        return 0;
+    for (uint32_t k0 = kPieceK0Min; k0 <= 16; k0++) {
+        const uint64_t units = n_tail * (((uint64_t)len + (1u << k0) - 1) >> k0);
+        if ((units + 64 / G - 1) / (64 / G) <= (uint64_t)c.cus * kWavesPerBlock) return k0;
+    }
+    return 0;
 }
 
 // Persistent waves take whole frame groups, so a launch lasts
@@ -530,6 +574,20 @@ val_status_t launch_uniform(const Ctx &c, FrameParams &p, uint32_t G, uint32_t l
     if (full > 0 && n_tail > 0)
         while (Gt < 64 && (n_tail + 64 / (2 * Gt) - 1) / (64 / (2 * Gt)) <= waves) Gt *= 2;
     if (Gt == G) return launch_uniform_one(c, p, G, len, s);
+    if (const uint32_t k0 = tail_piece_k0(c, p, G, len, n_tail)) {
+        FrameParams m = p;
+        m.n = (uint32_t)n_main;
+        m.tail_n = (uint32_t)n_tail;
+        m.tail_k0 = k0;
+        m.tail_units = (uint32_t)(((uint64_t)len + (1u << k0) - 1) >> k0);
+        if (!p.off) {
+            m.last_len = p.flen;  // frame n_main - 1 is a full one
+            m.tail_last_len = p.last_len;
+        }
+        const val_status_t st = launch_uniform_one(c, m, G, len, s);
+        if (st == VAL_OK) g_tail_piece_launches.fetch_add(1, std::memory_order_relaxed);
+        return st;
+    }
     FrameParams m = p, t = p;
     m.n = (uint32_t)n_main;
     t.n = (uint32_t)n_tail;
@@ -560,6 +618,7 @@ void scratch_free(StreamScratch *x)
 {
     arena_free(x->region);
     arena_free(x->queue);
+    arena_free(x->tail);
     arena_free(x->bin);
     if (x->done) (void)hipEventDestroy(x->done);
     delete x;
@@ -1900,6 +1959,10 @@ void val_gpu_set_host_cpu_threads(uint32_t threads)
 }
 
 uint64_t val_gpu_host_multi_min_bytes(int devices) { return host_multi_min_bytes(devices); }
+
+void val_gpu_set_tail_pieces(int enable) { g_tail_pieces.store(enable < 0 ? -1 : (enable ? 1 : 0)); }
+
+uint64_t val_gpu_tail_piece_launches(void) { return g_tail_piece_launches.load(std::memory_order_relaxed); }
 
 uint64_t val_gpu_host_multi_min_bytes_ex(int devices, int pinned, uint64_t mean_len)
 {
