@@ -88,7 +88,8 @@ def main():
     s["bench_line_cfg3"] = bench_line(os.path.join(o, "bench.json"))
     s["other_bench_lines"] = [b for b in (bench_line(os.path.join(o, f"bench_{k}.json"))
                                           for k in ("verify", "cfg4", "cfg2", "cfg5")) if b]
-    s["rocprof_cfg3"] = kernel_trace(o, "trace", rnd, "cfg3")
+    # the headline's own kernel (8 lanes per 16,400-B frame); the cfg4 block and its proxy add more G = 16 time
+    s["rocprof_cfg3"] = kernel_trace(o, "trace", rnd, "cfg3", prefer="k_frames<8, 1, false, false")
     s["rocprof_cfg5"] = kernel_trace(o, "trace5", rnd, "cfg5", prefer="k_frames_ragged")
     s["pmc_traffic_cfg3"] = traffic(o, "pmc_fetch", "pmc_write", "cfg3", "pmc_cfg3.json")
     s["pmc_traffic_cfg3_verify"] = traffic(o, "pmc_fetch_v", None, "cfg3_verify", "pmc_cfg3_verify.json")
