@@ -42,6 +42,11 @@ def workload(name, dev):
         n, L = {"cfg2": (1 << 16, 1040), "cfg4": (131113, 65532), "w256": (256, 1040)}[name]
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    if name == "cfg3d":  # cfg3's layout (1 M x 16,400 B at stride 16,404) through descriptors with the hint
+        n, L = 1 << 20, 16400
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        off = torch.arange(n, device=dev, dtype=torch.int64) * (L + 4)
+        return dict(buf=buf, off=off, length=torch.full((n,), L, dtype=torch.int32, device=dev), len_hint=L), n * L
     if name == "cfg4d":  # cfg4 as bench.py launches it: descriptors with the uniform length hint
         n, L = 131113, 65532
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

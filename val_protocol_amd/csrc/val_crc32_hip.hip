@@ -454,8 +454,8 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     // with 64). Groups under 128 KiB pull from 64 partitions: descriptor groups
     // from 16 KiB (u4200d +4%, u1100d +6%; with one word they lost up to 2x),
     // strided ones from 32 KiB (s4200 +3%; s1100's 17.6 KiB groups -3%);
-    // descriptor groups of 128-192 KiB stay static (u16400d -1% either way):
-    // profiles/r02_ab_dynparts.log.
+    // descriptor groups of 128-192 KiB stay static below 16 rounds (u16400d
+    // -1% either way: profiles/r02_ab_dynparts.log) and take one word above.
     const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * wpb);
     p.qhead = nullptr;
     const uint64_t group_bytes = (uint64_t)(64 / G) * len;
@@ -471,7 +471,15 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
 #ifndef VCRC_DYN_MIN_GROUP_PARTS_DESC
 #define VCRC_DYN_MIN_GROUP_PARTS_DESC (16u << 10)
 #endif
-    const bool one_word = group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_DESC : VCRC_DYN_MIN_GROUP);
+    // Descriptor groups of 128-192 KiB take the one-word queue only from 16
+    // rounds on: cfg3's layout through descriptors (32 rounds) +3.0%, 3 GB of
+    // 16,400-B frames (6 rounds) -2.8% with it (profiles/r06_ab_desc_dyn_tail.log).
+#ifndef VCRC_DYN_DESC_LONG_ROUNDS
+#define VCRC_DYN_DESC_LONG_ROUNDS 16
+#endif
+    const bool one_word = group_bytes >= (p.off ? (rounds >= VCRC_DYN_DESC_LONG_ROUNDS ? VCRC_DYN_MIN_GROUP
+                                                                                       : VCRC_DYN_MIN_GROUP_DESC)
+                                                : VCRC_DYN_MIN_GROUP);
     const bool parts =
         group_bytes >= (p.off ? VCRC_DYN_MIN_GROUP_PARTS_DESC : VCRC_DYN_MIN_GROUP_PARTS) && group_bytes < VCRC_DYN_MIN_GROUP;
     // the queue's scratch may be dropped by scratch_for (another stream's call)
