@@ -3,6 +3,6 @@
 set -o pipefail
 O=gpurun_out/r6j
 mkdir -p $O
-timeout -k 10 600 python tools/ab_libs.py build/libA_r6.so build/libB_r6.so cfg3d u16400d cfg3b cfg4d cfg3d > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 4; }
+timeout -k 10 600 python tools/ab_libs.py build/libA_r6.so val_protocol_amd/libval_crc_hip.so cfg3d u16400d cfg3b cfg4d cfg3d > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 4; }
 cat $O/ab.log
 bash tools/gpu_round_profile.sh
