@@ -8,6 +8,7 @@
 #         cpu_crc32.c instrumented as well), one batched transfer at window 32
 #         over a transport whose recv returns 1..3000 bytes (random per call),
 #         then four at once
+#   both: the round-6 fault runs (sendfail, oversize, stale recv_buffer calls)
 # usage: bash tools/sanitize_sessions.sh tsan|asan OUTDIR   (needs /root/reference
 # and a built library). Prints the harness's JSON lines; the sanitizers'
 # reports go to OUTDIR/report.txt.
@@ -35,5 +36,11 @@ export TSAN_OPTIONS="exitcode=0 log_path=$O/san" ASAN_OPTIONS="detect_leaks=0 lo
 if [ "$MODE" = asan ]; then
   VAL_HARNESS_PARTIAL=r3000 VAL_HARNESS_SEED=7 "$O/harness" "$O/libval_san.so" loopback-batched 1048576 4096 32 2>> "$O/stderr.txt" | tail -1
 fi
+# round 6: the batcher's fault contracts (a failed send in a window and the
+# transfer after it, an oversize header and the transfer after it, stale
+# recv_buffer calls against an armed answer)
+VAL_HARNESS_MAX_TIMEOUT_MS=600 "$O/harness" "$O/libval_san.so" sendfail 1048576 1024 8 20 1 2>> "$O/stderr.txt" | tail -1
+VAL_HARNESS_MAX_TIMEOUT_MS=600 "$O/harness" "$O/libval_san.so" oversize 1048576 1024 8 100 1 2>> "$O/stderr.txt" | tail -1
+VAL_HARNESS_STALE_ARM=1 "$O/harness" "$O/libval_san.so" loopback-batched 1048576 1024 8 2>> "$O/stderr.txt" | tail -1
 "$O/harness" "$O/libval_san.so" loopback-batched-par 2000000 4096 32 4 2>> "$O/stderr.txt" | tail -1
 cat "$O"/san.[0-9]* "$O/stderr.txt" > "$O/report.txt" 2>/dev/null || :
