@@ -126,5 +126,9 @@ int main(int argc, char **argv)
            "\"cpu_fallbacks\":%llu,\"devices\":%d}\n",
            k, g_iters, (unsigned long long)g_seed, g_checked, g_bad, (unsigned long long)val_gpu_cpu_batch_count(),
            (unsigned long long)val_gpu_cpu_fallback_count(), val_gpu_device_count());
+    fflush(stdout);
+    /* device memory released while the HIP runtime is still loaded (ASAN's
+     * device allocator refuses frees that arrive after it has unloaded) */
+    val_gpu_shutdown();
     return g_bad ? 1 : 0;
 }
