@@ -486,8 +486,20 @@ def test_batched_sessions_under_sanitizers(tmp_path, mode):
     lines = [json.loads(ln) for ln in r.stdout.strip().splitlines()]
     par = lines[-1]
     assert len(par["runs"]) == 4 and par["lib_cpu_fallbacks"] == 0
-    runs = par["runs"] + lines[:-1]
-    assert len(runs) == (5 if mode == "asan" else 4)
+    faults = {ln["mode"]: ln for ln in lines[:-1] if ln.get("mode") in ("sendfail", "oversize")}
+    runs = par["runs"] + [ln for ln in lines[:-1] if ln.get("mode") not in ("sendfail", "oversize")]
+    assert sorted(faults) == ["oversize", "sendfail"] and len(lines) == len(faults) + len(runs) - 3
+    # the fault runs (round 6): the first transfer fails, the one after it on
+    # the same batchers completes with the file intact
+    for f in faults.values():
+        assert f["tx_status1"] != VAL_OK and f["tx_status2"] == VAL_OK and f["rx_status2"] == VAL_OK, f
+        assert f["equal2"] == 1, f
+    assert faults["sendfail"]["batch"][0]["failures"] >= 1
+    assert faults["oversize"]["batch"][1]["resyncs"] >= 1
+    # the stale-recv_buffer run: every probe answered directly, none wrong
+    stale = [r for r in runs if r.get("stale_probes")]
+    assert len(stale) == 1 and stale[0]["stale_wrong"] == 0 and stale[0]["stale_probes"] >= 1000
+    assert len(runs) == (6 if mode == "asan" else 5)
     for run in runs:
         assert run["tx_status"] == VAL_OK and run["rx_status"] == VAL_OK and run["equal"] == 1, run
         assert run["batch"][1]["rx_batched_answers"] >= (1 << 20) // (4096 - 12)

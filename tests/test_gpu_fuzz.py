@@ -2,7 +2,8 @@
 strided / descriptor-uniform / binned ragged / zero-copy / chunked, TX and
 verify, payload states, several logical GPUs, regions with random seeds),
 each call checked bit-exact against the oracle. Seeded, so a
-failure names a reproducible case; FUZZ_ROUNDS scales it."""
+failure names a reproducible case; FUZZ_ROUNDS scales it and FUZZ_SEED
+reseeds it."""
 import os
 
 import numpy as np
@@ -52,12 +53,14 @@ def _batch(rng):
 
 def test_fuzz_batches(vc, monkeypatch):
     dev = torch.device("cuda:0")
-    rng = np.random.default_rng(20261016)
+    rng = np.random.default_rng(int(os.environ.get("FUZZ_SEED", "20261016")))
     for r in range(ROUNDS):
         base, offs, lens = _batch(rng)
         n = offs.size
         want, want_h = _oracle.frames(base, offs, lens, header=True)
         case = f"round {r} n={n} lens {int(lens.min())}..{int(lens.max())}"
+        if r % 50 == 0:
+            print(case, flush=True)
         vc.set_geometry(int(rng.choice([0, 0, 0, 1, 2, 4, 8, 16, 32, 64])), int(rng.choice([-1, -1, 0, 1, 2])))
         vc.set_host_chunk_bytes(int(rng.choice([0, 0, 1 << 16, 1 << 20])))
         if rng.random() < 0.5:

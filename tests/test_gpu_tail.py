@@ -177,3 +177,93 @@ def test_forced_lanes_and_the_path_off_for_others(vc):
         assert used == expect, G
         want = _oracle.frames_strided(buf.cpu().numpy(), stride, flen, n, nthreads=16)
         assert np.array_equal(_u32(on), want) and np.array_equal(_u32(off), want), G
+
+
+def test_tail_fuzz(vc):
+    """Random uniform batches around the path's edges, each bit-exact against
+    the oracle with the path on and off: frame length 8-64 KiB, 1-3 full
+    rounds, 1 .. one round minus one tail frames, strided or descriptor
+    (unaligned start, one short and one empty frame among the tail frames),
+    header_crc, then verify with one corrupted tail frame. TAIL_FUZZ_CASES and
+    TAIL_FUZZ_SEED scale and reseed it."""
+    import os
+
+    cases = int(os.environ.get("TAIL_FUZZ_CASES", "4"))
+    rng = np.random.default_rng(int(os.environ.get("TAIL_FUZZ_SEED", "20261018")))
+    used_total = 0
+    for c in range(cases):
+        flen = int(rng.integers(8192, 65537))
+        G = vc.lanes_per_frame(flen)
+        assert G in (8, 16), flen
+        per_round = _waves() * (64 // G)
+        rounds = int(rng.integers(1, 4)) if flen <= 32768 else int(rng.integers(1, 3))
+        tail = int(rng.integers(1, per_round))
+        n = per_round * rounds + tail
+        case = f"case {c}: flen {flen} G {G} rounds {rounds} tail {tail}"
+        stride = flen + 4
+        g = torch.Generator(device=DEV).manual_seed(int(rng.integers(1 << 62)))
+        strided = bool(rng.random() < 0.5)
+        case += " strided" if strided else " descriptor"
+        if strided:
+            buf = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=DEV, generator=g)
+            hdr = torch.empty(n, dtype=torch.int32, device=DEV)
+
+            def fn():
+                return vc.frames(buf, stride=stride, flen=flen, n=n, out_hdr=hdr).clone(), hdr.clone()
+
+            host = buf.cpu().numpy()
+            want, want_h = _oracle.frames_strided(host, stride, flen, n, header=True, nthreads=16)
+            offs = np.arange(n, dtype=np.uint64) * stride
+            lens = np.full(n, flen, np.uint32)
+        else:
+            lens = np.full(n, flen, np.uint32)
+            lens[n - 1 - int(rng.integers(0, tail))] = int(rng.integers(1, flen))
+            lens[n - 1 - int(rng.integers(0, tail))] = 0
+            wire = lens.astype(np.int64) + 4 + rng.integers(0, 3, n)
+            first = int(rng.integers(0, 16))
+            offs = np.concatenate([[first], first + np.cumsum(wire)[:-1]]).astype(np.uint64)
+            buf = torch.randint(0, 256, (int(offs[-1]) + int(wire[-1]) + 8,), dtype=torch.uint8, device=DEV,
+                                generator=g)
+            d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+            d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+            hdr = torch.empty(n, dtype=torch.int32, device=DEV)
+
+            def fn():
+                return vc.frames(buf, off=d_off, length=d_len, len_hint=flen, out_hdr=hdr).clone(), hdr.clone()
+
+            host = buf.cpu().numpy()
+            want, want_h = _oracle.frames(host, offs, lens, header=True, nthreads=16)
+        (on, hon), (off_, hoff), used = _run_both(vc, fn)
+        used_total += used
+        assert np.array_equal(_u32(on), want) and np.array_equal(_u32(off_), want), case
+        assert np.array_equal(_u32(hon), want_h) and np.array_equal(_u32(hoff), want_h), case
+        # verify: trailers from the oracle, one tail frame with a flipped bit
+        for o, L, w in zip(offs[n - tail:], lens[n - tail:], want[n - tail:]):
+            host[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(int(w).to_bytes(4, "little"), np.uint8)
+        # the main rounds' trailers too, vectorised for the strided layout
+        if strided:
+            rows = host[:(n - tail) * stride].reshape(n - tail, stride)
+            rows[:, flen:] = want[:n - tail].astype("<u4").view(np.uint8).reshape(n - tail, 4)
+        else:
+            for o, L, w in zip(offs[:n - tail], lens[:n - tail], want[:n - tail]):
+                host[int(o) + int(L):int(o) + int(L) + 4] = np.frombuffer(int(w).to_bytes(4, "little"), np.uint8)
+        bad = n - tail + int(rng.integers(0, tail))
+        host[int(offs[bad]) + int(rng.integers(0, int(lens[bad]) + 4))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        d = torch.from_numpy(host).to(DEV)
+        d_off = torch.from_numpy(offs.view(np.int64)).to(DEV)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(DEV)
+
+        def vfn():
+            ok, nbad = vc.verify_frames(d, off=d_off, length=d_len, len_hint=flen)
+            return ok.cpu().numpy(), int(nbad.item())
+
+        (ok_on, nb_on), (ok_off, nb_off), vused = _run_both(vc, vfn)
+        used_total += vused
+        want_ok = np.ones(n, np.uint8)
+        want_ok[bad] = 0
+        assert nb_on == nb_off == 1, case + " verify"
+        assert np.array_equal(ok_on, want_ok) and np.array_equal(ok_off, want_ok), case + " verify"
+        print(f"{case}: tail-piece launches {used}+{vused}", flush=True)
+        del buf, d, host
+        torch.cuda.empty_cache()
+    assert used_total >= 1 or cases < 3  # about half the cases take the path (tails under ~half a round)
