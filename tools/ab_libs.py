@@ -67,6 +67,11 @@ def workload(name, dev):
         n, L = (int(v) for v in name[1:].split("x"))
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
         return dict(buf=buf, stride=L + 4, flen=L, n=n), n * L
+    if name.startswith("d") and "x" in name:  # dNNNxLLLLL: NNN frames of LLLLL CRC bytes, descriptors with the hint
+        n, L = (int(v) for v in name[1:].split("x"))
+        buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)
+        off = torch.arange(n, device=dev, dtype=torch.int64) * (L + 4)
+        return dict(buf=buf, off=off, length=torch.full((n,), L, dtype=torch.int32, device=dev), len_hint=L), n * L
     if name.startswith("s") and name[1:].isdigit():  # sNNNNN: 1 M strided frames of NNNNN CRC bytes, stride +4
         n, L = 1 << 20, int(name[1:])
         buf = torch.randint(0, 256, (n * (L + 4),), dtype=torch.uint8, device=dev, generator=g)

@@ -798,7 +798,14 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
                     // then holds a reserved long group while others run dry)
         for (;;) {
             uint32_t k = 0;
+#ifdef VCRC_DYN_PRECHECK
+            if (ql == 0) {
+                k = __hip_atomic_load(&p.qhead[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (dyn + (uint64_t)k * kGroups < p.n) k = atomicAdd(&p.qhead[0], 1u);
+            }
+#else
             if (ql == 0) k = atomicAdd(&p.qhead[0], 1u);
+#endif
             k = __builtin_amdgcn_readfirstlane(k);
             const uint64_t gb = dyn + (uint64_t)k * kGroups;
             if (gb >= p.n) break;
@@ -837,9 +844,14 @@ __global__ __launch_bounds__(BT) void k_frames(const FrameParams p)
         if (p.tail_n) tail_pieces<G, PF, C0>(p, ql, sb);
     }
     VCRC_STAMP(2);
-    if (ql == 0) {
+    // Exits are counted per workgroup, after a barrier: one atomic per CU. One
+    // per wave (4,096 on one word, serialised at its atomic unit) added tens of
+    // microseconds to the end of short launches, where the waves all finish
+    // together.
+    __syncthreads();
+    if (threadIdx.x == 0) {
         const uint32_t out = atomicAdd(&p.qhead[kDynParts * 16u], 1u);
-        if (out == (uint32_t)nwaves - 1u) {  // every wave is past its last dequeue
+        if (out == gridDim.x - 1u) {  // every wave is past its last dequeue
             for (uint32_t i = 0; i < P; i++) atomicExch(&p.qhead[i * 16u], 0u);
             atomicExch(&p.qhead[kDynParts * 16u], 0u);
         }

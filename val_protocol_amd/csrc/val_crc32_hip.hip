@@ -374,8 +374,21 @@ hipError_t launch_uniform_g(int pf, dim3 grid, hipStream_t s, const FrameParams 
 val_status_t arena_acquire(Arena &a, size_t bytes, hipStream_t s, uint8_t **out);
 
 // Dynamic tail of long uniform launches (k_frames): VAL_GPU_DYNAMIC_TAIL=0/1.
-#ifndef VCRC_DYN_MIN_ROUNDS
-#define VCRC_DYN_MIN_ROUNDS 4
+// A launch takes it when it is long enough for the queue to pay: 8 or 16
+// lanes per frame from 1.45 MiB of frames per wave (about 6 GB at 4,096
+// waves), 2 or 4 lanes from 8 group rounds. Shorter launches measured faster
+// static, once the exits were counted per workgroup (same box, back to back,
+// profiles/r06_ab_dyn_tail_rules.log): 64 KiB frames 4 / 5 rounds -2.5 /
+// -0.6% with the queue, 6 / 7 rounds +0.5 / +1.0%; 16,400-B frames 6 / 8
+// rounds -3.7 / -1.6%, 12 / 16 rounds +0.5 / +1.6%; 4,200-B frames (8 lanes,
+// 34 KiB groups) 4 / 8 / 12 rounds -8 / -5 / -3.6%; 1,100-B and 2,000-B frames
+// at 4 rounds -5% and -3.9%, 600-B and 1,100-B frames at 8 rounds +3.6% and
+// +3.2%.
+#ifndef VCRC_DYN_MIN_WAVE_BYTES
+#define VCRC_DYN_MIN_WAVE_BYTES 1520000u
+#endif
+#ifndef VCRC_DYN_MIN_ROUNDS_SHORT
+#define VCRC_DYN_MIN_ROUNDS_SHORT 8
 #endif
 #ifndef VCRC_DYN_TAIL_DEFAULT
 #define VCRC_DYN_TAIL_DEFAULT 1
@@ -452,10 +465,11 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
     // about 48 dequeues/us at 6 TB/s, under the ~88/us one word serves, and
     // one word evens the end out better than partitions (cfg3 -1.5%, cfg4 -3.7%
     // with 64). Groups under 128 KiB pull from 64 partitions: descriptor groups
-    // from 16 KiB (u4200d +4%, u1100d +6%; with one word they lost up to 2x),
+    // from 16 KiB (round 2: u4200d +4%, u1100d +6%; with one word they lost up to 2x),
     // strided ones from 32 KiB (s4200 +3%; s1100's 17.6 KiB groups -3%);
     // descriptor groups of 128-192 KiB stay static below 16 rounds (u16400d
     // -1% either way: profiles/r02_ab_dynparts.log) and take one word above.
+    // Which launches are long enough for any queue: VCRC_DYN_MIN_WAVE_BYTES above.
     const uint64_t rounds = ((uint64_t)p.n + 64 / G - 1) / (64 / G) / (blocks * wpb);
     p.qhead = nullptr;
     const uint64_t group_bytes = (uint64_t)(64 / G) * len;
@@ -498,7 +512,9 @@ val_status_t launch_uniform_one(const Ctx &c, FrameParams &p, uint32_t G, uint32
         a.counts_zero = false;  // set again once the launch is queued (its last pieces re-zero the pairs)
         p.tail_acc = reinterpret_cast<uint32_t *>(q);
     }
-    if (dyn_tail_enabled() && rounds >= VCRC_DYN_MIN_ROUNDS && (one_word || parts)) {
+    const bool long_enough = G >= 8 ? rounds * group_bytes >= (uint64_t)VCRC_DYN_MIN_WAVE_BYTES
+                                    : rounds >= VCRC_DYN_MIN_ROUNDS_SHORT;
+    if (dyn_tail_enabled() && long_enough && (one_word || parts)) {
         if (!used) used = &scratch_for(cm, s);
         Arena &a = used->queue;
         uint8_t *q = nullptr;
